@@ -1,0 +1,96 @@
+/* rt_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C) of the reference ray tracer's hot path, used as the parity checker and
+ * as the `cpu_baseline` ("port") in bench.py. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library. The product (ray-tracing-project_amd/) never links it.
+ *
+ * Reference followed (plindhorst/Ray-Tracing-Project, read-only at /root/reference):
+ *   src/flyscene.cpp:250-614   raytraceScene / traceRay / calculateMinimumFace / calculateDistance /
+ *                              intersectBox / shadow / calcSingleColor / interpolateNormal / calculateColor
+ *   src/BoundingBox.cpp:1-228  flat box partition (fitMesh/fitFaces/splitBox/outsideFaces/average)
+ *   src/flyscene.cpp:399-428   generateBoundingBoxes pass loop
+ *   tucano/utils/objimporter.hpp:81-351, utils/mtlIO.hpp:49-140  OBJ/MTL ingest
+ *   tucano/mesh.hpp:448-482,592-644, model.hpp:102-105,169-173   face normals, normalisation
+ *   tucano/camera.hpp:115-118,155-173,263-266, utils/flycamera.hpp:76-202  ray generation
+ *
+ * Arithmetic follows Eigen 3.3.7's evaluation order; pinned bit-for-bit by tests/golden/eigen_kat.bin
+ * (generated from the reference's vendored Eigen by oracle/eigen_kat.cpp) and by the reference-run
+ * known-answer values in SURVEY.md Appendix C (tests/golden/survey_kat.json).
+ */
+#ifndef RT_ORACLE_H
+#define RT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_mesh orc_mesh;
+typedef struct orc_scene orc_scene;
+
+/* material parameter block: ka[3] kd[3] ks[3] Ns Ni d  (12 floats) */
+#define ORC_MAT_FLOATS 12
+
+int orc_mesh_load_obj(const char* path, orc_mesh** out);
+int orc_mesh_from_arrays(int32_t nv, const float* v3, const float* vn3_or_null, int32_t n_groups,
+                         const int32_t* group_index_counts, const uint32_t* indices,
+                         const int32_t* group_material, int32_t n_materials, const float* mat12,
+                         orc_mesh** out);
+void orc_mesh_free(orc_mesh* m);
+void orc_mesh_counts(const orc_mesh* m, int32_t* nv, int32_t* nf, int32_t* nm);
+/* any pointer may be NULL. v4:[nv][4] vn3:[nv][3] fidx:[nf][3] fn3:[nf][3] fmat:[nf] mats:[nm][12]
+ * M16: shape-model matrix (column-major 4x4), sc4: normalization scale + object centre */
+void orc_mesh_export(const orc_mesh* m, float* v4, float* vn3, uint32_t* fidx, float* fn3,
+                     int32_t* fmat, float* mats, float* M16, float* sc4);
+
+/* deterministic synthetic soup (C3/C4): SplitMix64(seed); see DESIGN.md "Scenes" */
+void orc_generate_soup(int32_t n_tris, uint64_t seed, float* v3_out /* [3n][3] */);
+
+int orc_scene_build(orc_mesh* m, int32_t min_faces, int32_t max_boxes, orc_scene** out);
+void orc_scene_free(orc_scene* s);
+int32_t orc_scene_box_count(const orc_scene* s);
+/* bounds6:[nb][6] (low xyz, high xyz, object space), counts:[nb], face_order:[nf] (box-major) */
+void orc_scene_boxes(const orc_scene* s, float* bounds6, int32_t* counts, int32_t* face_order);
+int32_t orc_scene_pass_counts(const orc_scene* s, int32_t* out, int32_t max);
+
+typedef struct orc_camera {
+  float view[16];    /* Affine3f view matrix, column-major */
+  float viewport[4]; /* x, y, w, h */
+  float fovy;
+  float aspect;
+} orc_camera;
+
+/* Flycamera at default pose after translate(dx,dy,dz) + updateViewMatrix() (flycamera.hpp:166-202) */
+void orc_camera_flycam(int32_t W, int32_t H, float dx, float dy, float dz, orc_camera* out);
+void orc_camera_ray(const orc_camera* c, int32_t i, int32_t j, float* o3, float* d3);
+
+typedef struct orc_render_opts {
+  int32_t max_depth;   /* reference max_depth (2 = FULL); PRIMARY uses 1 */
+  int32_t shadows;     /* 1 = shadow() any-hit per light (FULL), 0 = disabled (PRIMARY) */
+  float background[3]; /* BACKGROUND_COLOR */
+  float def_mat[ORC_MAT_FLOATS]; /* Flyscene default ka/kd/ks/shininess/.. (flyscene.hpp:179-184) */
+} orc_render_opts;
+
+void orc_render_opts_default(orc_render_opts* o, int32_t full);
+
+/* Render W x H (pixels==NULL) or a list of n_pixels (i,j) pairs. rgb:[n][3], face:[n] (-1 miss), t:[n]
+ * outputs may be NULL. Threads interleave rows (deterministic). Returns 0 on success. */
+int orc_render(orc_scene* s, const orc_camera* cam, const float* lights6, int32_t n_lights, int32_t W,
+               int32_t H, const orc_render_opts* opts, int32_t n_pixels, const int32_t* pixels,
+               int32_t nthreads, float* rgb, int32_t* face, float* t);
+
+/* calculateMinimumFace for n rays; face -1 = miss (t = +inf) */
+int orc_closest(orc_scene* s, int32_t n, const float* o3, const float* d3, int32_t* face, float* t,
+                float* P3);
+/* shadow(P, L) for n rays: out 1 = blocked */
+int orc_shadow(orc_scene* s, int32_t n, const float* P3, const float* L3, int32_t* out);
+
+/* Eigen-order primitive known-answer entry point (op codes as in oracle/eigen_kat.cpp) */
+int orc_kat(int32_t op, int32_t n, const float* in, float* out);
+
+const char* orc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
