@@ -1,0 +1,48 @@
+# Top-level build: the product library (gfx950 HIP + host C++) and the test oracle.
+#   make            -> ray-tracing-project_amd/lib/librtamd.so, oracle/build/liboracle.so, CLI
+# Float semantics: -ffp-contract=off everywhere (no FMA contraction; the reference rounds every op),
+# hipcc's default correctly rounded fp32 division / sqrt kept, no fast-math.
+PKG      := ray-tracing-project_amd
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+HIPFLAGS := -O3 --offload-arch=$(ARCH) -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+            -munsafe-fp-atomics -Wall -Wno-unused-function -Wno-unused-variable
+CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+OBJ      := $(PKG)/build
+LIB      := $(PKG)/lib/librtamd.so
+HDRS     := include/rt/rt_api.h $(wildcard $(PKG)/csrc/*.h)
+
+all: $(LIB) oracle cli
+
+$(OBJ)/rt_device.o: $(PKG)/csrc/rt_device.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/rt_host.o: $(PKG)/csrc/rt_host.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o
+	@mkdir -p $(PKG)/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+cli: $(PKG)/lib/rt_render_cli
+
+$(PKG)/lib/rt_render_cli: $(PKG)/host/main.cpp $(PKG)/host/flyscene.cpp $(PKG)/host/flyscene.hpp $(LIB)
+	$(CXX) $(CXXFLAGS) -Iinclude -o $@ $(PKG)/host/main.cpp $(PKG)/host/flyscene.cpp \
+	    -L$(PKG)/lib -lrtamd -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: $(PKG)/csrc/rt_device.hip $(HDRS)
+	@mkdir -p $(OBJ)/asm
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(OBJ)/asm/rt_device.s $<
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -Rpass-analysis=kernel-resource-usage -o /dev/null $< 2> $(OBJ)/asm/resource.txt || true
+
+clean:
+	rm -rf $(OBJ) $(PKG)/lib
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle cli asm clean

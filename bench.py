@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X ray-traversal hot path (BASELINE.json metric).
+
+Metric: "Mrays/s (primary) + frame ms at 1920x1080, 1M-tri BVH, 1/2/4/8 GPU".
+Workload (C3): 1,000,000 random triangles (SplitMix64 seed 12345), Flycamera eye
+(0,0,1) (translate(0,0,20)), fovy 60, one white light at (-0.5,2,3), PRIMARY mode (closest hit +
+unshadowed Phong). A step = one frame: one launch of the render kernel over this rank's 8x8 tiles.
+Scene and frame buffer are resident in HBM before the timed region; no host copies inside it.
+
+Multi-GPU (one process per GPU, torchrun): the frame grows with N at 16:9 so that every GPU traces a
+1080p-equivalent share (weak scaling; N=4 is C4's 3840x2160); tiles are interleaved over ranks, the
+scene is replicated, and there is no collective on the data path (barrier + max/sum reductions of the
+timing only). `--frame WxH` fixes the frame instead (strong scaling, e.g. --frame 3840x2160).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including:
+  roofline: algorithmic bytes per ray B = 64*N_node + 40*N_tri + 92*hit + 12 from a
+            counting run of the same kernel on the same frame, times rays per launch, over the average
+            launch duration measured with HIP events on the library's stream; peak 8 TB/s HBM3E.
+  cpu_baseline: the CPU restatement of the reference algorithm (oracle/, "port") on a bounded pixel
+            sample of the same frame, timed on this host's cores.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "ray-tracing-project_amd")
+
+
+def load_rtamd():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rtamd", os.path.join(PKG, "rtamd.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def frame_for(n_gpus, override):
+    if override:
+        w, h = override.lower().split("x")
+        return int(w), int(h), "strong"
+    s = math.sqrt(n_gpus)
+    return 8 * round(1920 * s / 8), 8 * round(1080 * s / 8), "weak"
+
+
+def cpu_baseline(rt_soup_args, W, H, target_s, threads):
+    """Oracle ("port" of the reference algorithm) on a strided pixel sample of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n_tris, seed, mat = rt_soup_args
+    v = O.generate_soup(n_tris, seed)
+    f = np.arange(3 * n_tris, dtype=np.uint32).reshape(-1, 3)
+    t0 = time.perf_counter()
+    sc = O.Scene(O.Mesh.from_arrays(v, f, np.array([mat], np.float32)))
+    build_s = time.perf_counter() - t0
+    cam = O.flycam(W, H, 0, 0, 20)
+
+    def run(step):
+        pix = np.array([(i, j) for j in range(step // 2, H, step) for i in range(step // 3, W, step)], np.int32)
+        t = time.perf_counter()
+        sc.render(cam, O.DEFAULT_LIGHTS, W, H, full=False, pixels=pix, threads=threads)
+        return len(pix), time.perf_counter() - t
+
+    n, dt = run(97)  # calibration sample
+    rate = n / max(dt, 1e-6)
+    step = max(2, int(math.sqrt(W * H / max(rate * target_s, 1.0))))
+    n, dt = run(step)
+    return {"value": round(n / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{n} primary rays = every {step}th pixel in x and y of the same {W}x{H} frame "
+                      f"(1M-tri scene, eye (0,0,1)); {dt:.1f} s of CPU work on {threads} threads; "
+                      f"box partition build {build_s:.1f} s excluded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--tris", type=int, default=1_000_000)
+    ap.add_argument("--frame", default=None, help="WxH (strong scaling); default 1080p per GPU (weak)")
+    ap.add_argument("--mode", choices=["primary", "full"], default="primary")
+    ap.add_argument("--scene", default="soup", help="soup | bunny")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-stats", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and world > 1:
+        print(f"warning: WORLD_SIZE {world} != --gpus {a.gpus}", file=sys.stderr)
+    n = max(world, 1)
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def reduce(x, op):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    rt = load_rtamd()
+    W, H, scaling = frame_for(n, a.frame)
+    t0 = time.perf_counter()
+    if a.scene == "soup":
+        mesh, _, _ = rt.soup_mesh(a.tris, 12345)
+        scene_name = f"{a.tris} random triangles (SplitMix64 seed 12345)"
+    else:
+        mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
+        scene_name = "Stanford bunny (69,451 triangles)"
+    sc = rt.Scene(mesh, device=local)
+    info = sc.info()
+    setup_s = time.perf_counter() - t0
+    cam = rt.flycam(W, H, 0, 0, 20)
+    mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY
+    shard = (rank, n)
+
+    for _ in range(a.warmup):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    sc.synchronize()
+
+    barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    st = sc.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+
+    my_rays = st["primary_rays"] * a.steps
+    elapsed_max = reduce(elapsed, dist.ReduceOp.MAX if dist else None)
+    total_rays = reduce(float(my_rays), dist.ReduceOp.SUM if dist else None)
+    kernel_ms_avg = st["kernel_ms"] / max(st["launches"], 1)
+    kernel_ms_max = reduce(kernel_ms_avg, dist.ReduceOp.MAX if dist else None)
+
+    roof = None
+    stats = None
+    if rank == 0 and not a.no_stats:
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard, flags=rt.RT_FRAME_STATS)
+        stats = sc.synchronize()
+        rays = max(stats["primary_rays"], 1)
+        n_node = stats["node_visits"] / rays
+        n_tri = stats["tri_tests"] / rays
+        hit = stats["hits"] / rays
+        b_ray = 64 * n_node + 40 * n_tri + 92 * hit + 12
+        achieved = b_ray * st["primary_rays"] / (kernel_ms_avg * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                "frac": round(achieved / 8000.0, 4), "traffic": None,
+                "bytes_per_ray": round(b_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
+                "hit": round(hit, 4), "kernel_ms": round(kernel_ms_avg, 4),
+                "wave_fetch_bytes_per_ray": round((64 * stats["wave_node_fetches"] + 64 * stats["wave_tri_fetches"]) / rays, 2)}
+
+    cpu = None
+    if rank == 0 and n == 1 and not a.no_cpu:
+        threads = min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline((a.tris, 12345, rt.SOUP_MATERIAL), W, H, a.cpu_seconds, threads)
+
+    if rank == 0:
+        value = total_rays / elapsed_max / 1e6
+        out = {
+            "metric": "Mrays/s (primary) + frame ms at 1920x1080, 1M-tri BVH, 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"C3: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light",
+                       "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
+                       "parallelism": f"tiles/{n} (8x8 tiles interleaved over ranks, scene replicated)",
+                       "kernel_ms_per_frame": round(kernel_ms_max, 4),
+                       "kernel_mrays_per_s": round(total_rays / a.steps / (kernel_ms_max * 1e-3) / 1e6, 2),
+                       "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
+                       "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+/* rt_api.h -- C ABI of the MI355X-native ray-traversal library (librtamd.so).
+ *
+ * Drop-in boundary for the reference's CPU render path (plindhorst/Ray-Tracing-Project):
+ *   Flyscene::raytraceScene(int width, int height)      src/flyscene.hpp:65, src/flyscene.cpp:250-297
+ *     -> traceRayThread (ray generation)                 src/flyscene.cpp:299-314
+ *     -> traceRay / calculateMinimumFace / shadow / calculateColor   src/flyscene.cpp:317-614
+ * The GL-free Flyscene mirror (ray-tracing-project_amd/host/flyscene.hpp) keeps initialize(w,h) and
+ * raytraceScene(w,h) and calls rt_render() for the whole frame, then writes result.ppm with
+ * rt_write_ppm() (= Tucano::ImageImporter::writePPMImage, tucano/utils/ppmIO.hpp:135-156).
+ *
+ * Conventions: plain C types only; every call returns 0 (RT_OK) or a negative rt_status; the message
+ * of the last failure on the calling thread is rt_last_error(). No exceptions cross the ABI. A scene
+ * handle is used from one host thread at a time. The caller owns every input array and output buffer;
+ * the library copies the scene to the device at rt_scene_create(). There is no CPU fallback: every
+ * render/trace entry point runs the gfx950 kernels and fails with RT_ERR_NO_DEVICE without a GPU.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_API_VERSION 1
+
+typedef enum rt_status {
+  RT_OK = 0,
+  RT_ERR_INVALID = -1,   /* bad argument / malformed input */
+  RT_ERR_IO = -2,        /* file could not be opened / written */
+  RT_ERR_NOMEM = -3,     /* host or device allocation failed */
+  RT_ERR_HIP = -4,       /* HIP runtime error (message in rt_last_error) */
+  RT_ERR_NO_DEVICE = -5, /* no GPU, or the scene was created host-only */
+  RT_ERR_UNSUPPORTED = -6
+} rt_status;
+
+/* Tucano::Material::Mtl fields the ray tracer reads (tucano/materials/mtl.hpp:22-40) */
+typedef struct rt_material {
+  float ka[3], kd[3], ks[3];
+  float shininess;        /* Ns */
+  float optical_density;  /* Ni */
+  float dissolve;         /* d  */
+} rt_material;
+
+/* ---------------------------------------------------------------------------------------------
+ * Host-side scene ingest with Tucano semantics (no GPU needed)
+ * ------------------------------------------------------------------------------------------- */
+typedef struct rt_mesh rt_mesh;
+
+/* Tucano::MeshImporter::loadObjFile (tucano/utils/objimporter.hpp:117-351) + Mesh::normalizeModelMatrix
+ * (tucano/model.hpp:169-173), as Flyscene::initialize does (src/flyscene.cpp:18-22). */
+int rt_mesh_load_obj(const char* path, rt_mesh** out);
+/* Same ingest from memory: v3 [nv][3]; vn3 [nv][3] or NULL (then normals are computed as
+ * computeNormals, objimporter.hpp:81-106); index groups as usemtl groups (group_index_counts are
+ * index counts, multiples of 3); materials [n_materials]. */
+int rt_mesh_from_arrays(int32_t n_vertices, const float* v3, const float* vn3, int32_t n_groups,
+                        const int32_t* group_index_counts, const uint32_t* indices,
+                        const int32_t* group_material, int32_t n_materials,
+                        const rt_material* materials, rt_mesh** out);
+void rt_mesh_destroy(rt_mesh* m);
+
+/* Borrowed view of a prepared mesh, in the layout Flyscene holds after initialize(). */
+typedef struct rt_mesh_desc {
+  int32_t n_vertices;
+  const float* vertices;            /* [n_vertices][4] object space, w = 1 (Mesh::vertices, mesh.hpp:292) */
+  const float* vertex_normals;      /* [n_vertices][3] (Mesh::normals, mesh.hpp:293)              */
+  int32_t n_faces;
+  const uint32_t* face_vertex_ids;  /* [n_faces][3] (Face::vertex_ids, mesh.hpp:242)              */
+  const float* face_normals;        /* [n_faces][3] (Face::normal, mesh.hpp:245; createFaces :475-477) */
+  const int32_t* face_material_ids; /* [n_faces] (Face::material_id), -1 = none                   */
+  int32_t n_materials;
+  const rt_material* materials;     /* Flyscene::materials (flyscene.hpp:151)                     */
+  float shape_model_matrix[16];     /* Mesh::getShapeModelMatrix(), column-major (model.hpp:102-105) */
+} rt_mesh_desc;
+
+int rt_mesh_get_desc(const rt_mesh* m, rt_mesh_desc* out);
+
+/* Deterministic synthetic triangle soup used by the C3/C4 workloads: n_tris triangles, unshared
+ * vertices v3_out [3*n_tris][3]; SplitMix64(seed); centres U[-0.5,0.5)^3, vertex jitter U[-0.01,0.01)^3. */
+void rt_generate_soup(int32_t n_tris, uint64_t seed, float* v3_out);
+
+/* Tucano::ImageImporter::writePPMImage (tucano/utils/ppmIO.hpp:135-156): P3, row 0 first,
+ * min(255, (int)(255*c)). rgb is [H][W][3]. */
+int rt_write_ppm(const char* path, const float* rgb, int32_t width, int32_t height);
+
+/* ---------------------------------------------------------------------------------------------
+ * Scene (device-resident acceleration structure)
+ * ------------------------------------------------------------------------------------------- */
+#define RT_DEVICE_NONE (-2) /* host-only scene: preparation + inspection, no upload, no rendering */
+
+typedef struct rt_scene_opts {
+  int32_t device;         /* HIP device ordinal; -1 = current device; RT_DEVICE_NONE = host only */
+  int32_t min_faces;      /* Flyscene::MIN_FACES (flyscene.hpp:168), default 300 */
+  int32_t max_boxes;      /* Flyscene::MAX_BOXES (flyscene.hpp:169), default INT32_MAX */
+  int32_t leaf_size;      /* BVH leaf size bound (1..16), 0 = default */
+  rt_material default_material; /* Flyscene::ka/kd/ks/shininess defaults (flyscene.hpp:179-184) */
+  float background[3];    /* Flyscene::BACKGROUND_COLOR (flyscene.hpp:175) */
+} rt_scene_opts;
+
+void rt_scene_opts_default(rt_scene_opts* o);
+
+typedef struct rt_scene rt_scene;
+
+/* Builds the reference's flat box partition (generateBoundingBoxes, flyscene.cpp:399-428, whose box
+ * order defines closest-hit tie-breaking) and the traversal BVH, then uploads both. */
+int rt_scene_create(const rt_mesh_desc* mesh, const rt_scene_opts* opts, rt_scene** out);
+void rt_scene_destroy(rt_scene* s);
+
+typedef struct rt_scene_info {
+  int32_t n_faces, n_vertices, n_ref_boxes;
+  int32_t bvh_nodes, bvh_leaves, bvh_depth;
+  int64_t device_bytes;
+  double build_ms;        /* host preparation (boxes + BVH) */
+  int32_t device;         /* RT_DEVICE_NONE for host-only scenes */
+} rt_scene_info;
+
+int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);
+/* reference boxes: bounds6 [n][6] (low xyz, high xyz, object space), counts [n], face_order [n_faces]
+ * (faces in reference iteration order: box creation order, then in-box order). NULL = skip. */
+int rt_scene_ref_boxes(const rt_scene* s, float* bounds6, int32_t* counts, int32_t* face_order);
+
+/* ---------------------------------------------------------------------------------------------
+ * Camera, lights, frames
+ * ------------------------------------------------------------------------------------------- */
+typedef struct rt_camera {
+  float view_matrix[16]; /* Camera::view_matrix (Affine3f), column-major (tucano/camera.hpp) */
+  float viewport[4];     /* Camera::viewport: x, y, width, height */
+  float fovy;            /* degrees */
+  float aspect_ratio;
+} rt_camera;
+
+/* Flycamera default pose (eye (0,0,2), tucano/utils/flycamera.hpp:76-86) after translate(dx,dy,dz)
+ * and updateViewMatrix(), with Flyscene::initialize's projection (fovy 60, aspect W/H, viewport). */
+void rt_camera_flycam(int32_t width, int32_t height, float dx, float dy, float dz, rt_camera* out);
+
+typedef struct rt_light {
+  float position[3]; /* Flyscene::lights[i].first  (flyscene.hpp:132) */
+  float color[3];    /* Flyscene::lights[i].second */
+} rt_light;
+
+#define RT_MAX_LIGHTS 16
+
+enum { RT_MODE_PRIMARY = 0, RT_MODE_FULL = 1 };
+
+typedef struct rt_frame {
+  int32_t width, height;
+  int32_t mode;        /* RT_MODE_PRIMARY: closest hit + unshadowed Phong (traceRay at depth limit 1);
+                          RT_MODE_FULL: reference traceRay as-is (shadow per light + 1 reflection) */
+  int32_t shard_index; /* this device renders the 8x8 tiles t with t % shard_count == shard_index */
+  int32_t shard_count; /* 1 = whole frame */
+  int32_t flags;       /* RT_FRAME_* */
+} rt_frame;
+
+#define RT_FRAME_WRITE_HITS 1 /* also record per-pixel face index and t (rt_frame_download) */
+#define RT_FRAME_STATS 2      /* counting run: per-ray node visits / triangle tests (slower) */
+
+typedef struct rt_stats {
+  double kernel_ms;         /* device time of the render kernels since the previous rt_synchronize,
+                               summed over launches (HIP events on the scene's stream) */
+  int64_t launches;         /* render launches covered by kernel_ms */
+  int64_t primary_rays;     /* pixels traced by this call */
+  int64_t total_rays;       /* primary + shadow + reflection rays issued */
+  int64_t hits;             /* primary rays that hit */
+  int64_t node_visits;      /* RT_FRAME_STATS: sum over rays of interior nodes whose box the ray hit */
+  int64_t tri_tests;        /* RT_FRAME_STATS: sum over rays of triangle tests */
+  int64_t wave_node_fetches;/* RT_FRAME_STATS: node records fetched (once per wave) */
+  int64_t wave_tri_fetches; /* RT_FRAME_STATS: triangle records fetched (once per wave) */
+} rt_stats;
+
+/* Renders the frame (this shard's tiles) on the scene's device and copies it into out_rgb
+ * ([H][W][3], row 0 = top, untouched outside this shard). Synchronous. */
+int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
+              const rt_frame* frame, float* out_rgb, rt_stats* stats);
+
+/* Device-resident variant for benchmarking: renders into the scene's device frame buffer and returns
+ * without synchronising; rt_synchronize() waits and fills the stats of the last render. */
+int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
+                    const rt_frame* frame);
+int rt_synchronize(rt_scene* s, rt_stats* stats);
+/* copies the last frame from the device: rgb [H][W][3]; face [H][W] (-1 miss) and t [H][W] need
+ * RT_FRAME_WRITE_HITS. NULL = skip. */
+int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t);
+
+/* calculateMinimumFace (flyscene.cpp:373-396) for n rays on the device: face -1 = miss (t = +inf) */
+int rt_trace_closest(rt_scene* s, int32_t n, const float* origins3, const float* dirs3, int32_t* face,
+                     float* t, float* P3);
+/* shadow(P, L) (flyscene.cpp:510-526) for n rays on the device: blocked 1/0 */
+int rt_trace_shadow(rt_scene* s, int32_t n, const float* P3, const float* L3, int32_t* blocked);
+
+/* ---------------------------------------------------------------------------------------------
+ * Misc
+ * ------------------------------------------------------------------------------------------- */
+int rt_device_count(void);       /* 0 when no GPU is visible */
+int rt_version(void);            /* RT_API_VERSION */
+const char* rt_last_error(void); /* thread-local */
+
+/* Verification hooks (tests only; never used by the render path): evaluate the Eigen-order float
+ * primitives of rt_math.h on the host (rt_debug_math_host) or in a gfx950 kernel
+ * (rt_debug_math_device) for n known-answer cases of op (tests/golden/eigen_kat.bin). */
+int rt_debug_math_host(int32_t op, int32_t n, const float* in, float* out);
+int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_API_H */

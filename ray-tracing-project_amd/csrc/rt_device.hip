@@ -1,0 +1,861 @@
+// rt_device.hip -- gfx950 kernels and device-side C ABI of the MI355X ray-traversal library.
+//
+// Hot path (reference: src/flyscene.cpp:299-614):
+//   one wave = one 8x8 pixel tile, one ray per lane; rays generated in registers (traceRayThread +
+//   Camera::screenToWorld, fp64 NDC as camera.hpp:159-162);
+//   wave-packet BVH traversal: every node record is fetched once per wave with a scalar load
+//   (s_load_dwordx16 of the 64-B node), each lane slab-tests both children, the wave descends by
+//   ballot (near child first by lane majority) and keeps ONE traversal stack for the wave (held in
+//   LDS or in the lanes of a VGPR -- template switch); lanes that cannot improve their
+//   hit simply vote "no", so the wave stays converged and only visits nodes some lane still needs;
+//   triangle test = the reference's calculateDistance/interpolateNormal arithmetic bit for bit
+//   (flyscene.cpp:444-478,572-600), tie-break by reference iteration rank (calculateMinimumFace
+//   keeps the first minimum, flyscene.cpp:381-391), plus the reference's own object-space box test
+//   (intersectBox, flyscene.cpp:484-507) for the candidate's reference box;
+//   shading = calculateColor/calcSingleColor (flyscene.cpp:542-614); FULL mode adds the shadow any-hit
+//   per light (flyscene.cpp:510-526) and the one reflection bounce of traceRay (flyscene.cpp:317-371).
+// No MFMA: there is no dense contraction in this path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "rt_kat.h"
+#include "rt_scene.h"
+
+using rt::f3;
+
+#define HIPCHECK(expr)                                                                   \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      rt::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return RT_ERR_HIP;                                                                 \
+    }                                                                                    \
+  } while (0)
+
+namespace rt {
+
+// ------------------------------------------------------------------------------------------------
+// uniform (scalar) loads: a generic pointer re-typed into the constant address space makes hipcc
+// emit s_load_dwordx16 for wave-uniform indices (one fetch per wave, data in SGPRs)
+// ------------------------------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) f4v* cf4p;
+
+template <typename T>
+__device__ __forceinline__ T sload64(const T* base, uint32_t i) {
+  static_assert(sizeof(T) == 64, "64-byte records");
+  const cf4p p = (cf4p)(base) + 4 * (size_t)i;
+  const f4v a = p[0], b = p[1], c = p[2], d = p[3];
+  T r;
+  __builtin_memcpy(reinterpret_cast<char*>(&r) + 0, &a, 16);
+  __builtin_memcpy(reinterpret_cast<char*>(&r) + 16, &b, 16);
+  __builtin_memcpy(reinterpret_cast<char*>(&r) + 32, &c, 16);
+  __builtin_memcpy(reinterpret_cast<char*>(&r) + 48, &d, 16);
+  return r;
+}
+__device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t i) { return sload64(base, i); }
+__device__ __forceinline__ TriRec64 sload_tri(const TriRec64* base, uint32_t i) { return sload64(base, i); }
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// counters of the RT_FRAME_STATS counting run
+enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_COUNT };
+
+struct Hit {
+  float t;
+  uint32_t rank;
+  uint32_t slot;
+};
+
+struct Ray {
+  f3 o, d;      // world space (triangle tests)
+  f3 id, oid;   // culling: 1/d (zeros nudged), -o/d
+  f3 o2, d2;    // object space (reference intersectBox): Minv*o_box, normalized(MS*d)
+};
+
+__device__ __forceinline__ float nudge(float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; }
+
+__device__ __forceinline__ void setup_cull(Ray& r) {
+  r.id = f3{__builtin_amdgcn_rcpf(nudge(r.d.x)), __builtin_amdgcn_rcpf(nudge(r.d.y)),
+            __builtin_amdgcn_rcpf(nudge(r.d.z))};
+  r.oid = f3{-r.o.x * r.id.x, -r.o.y * r.id.y, -r.o.z * r.id.z};
+}
+
+// Conservative slab test for one padded child box (culling only; exactness comes from padding)
+__device__ __forceinline__ float slab(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
+                                      float tmax_ray, bool& hit) {
+  const float tx0 = __builtin_fmaf(lx, r.id.x, r.oid.x), tx1 = __builtin_fmaf(hx, r.id.x, r.oid.x);
+  const float ty0 = __builtin_fmaf(ly, r.id.y, r.oid.y), ty1 = __builtin_fmaf(hy, r.id.y, r.oid.y);
+  const float tz0 = __builtin_fmaf(lz, r.id.z, r.oid.z), tz1 = __builtin_fmaf(hz, r.id.z, r.oid.z);
+  const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_ray));
+  hit = tmin <= tmax;
+  return tmin;
+}
+
+// The reference's object-space box test, exact (flyscene.cpp:484-507)
+__device__ __forceinline__ bool ref_box_test(const Ray& r, const float* bx) {
+  const float lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[4], bx[5], bx[6]};
+  const float o2[3] = {r.o2.x, r.o2.y, r.o2.z}, d2[3] = {r.d2.x, r.d2.y, r.d2.z};
+  float tin3[3], tout3[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float a = (lo[k] - o2[k]) / d2[k];
+    const float b = (hi[k] - o2[k]) / d2[k];
+    tin3[k] = smin(a, b);
+    tout3[k] = smax(a, b);
+  }
+  const float tin = smax(tin3[0], smax(tin3[1], tin3[2]));
+  const float tout = smin(tout3[0], smin(tout3[1], tout3[2]));
+  return !(tin > tout || tout < 0);
+}
+
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+
+// Rare path of a candidate (uniform triangle): interpolated normal non-zero (calculateDistance's
+// norm()==0 check, flyscene.cpp:467) and the reference box predicate. All loads wave-uniform.
+__device__ __forceinline__ bool accept_candidate(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0, f3 a1,
+                                                f3 a2, const Ray& r) {
+  const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
+  const float area = norm(cross(e0, neg(e2))) / 2;
+  const uint32_t* fs = P.fshade + 4 * (size_t)tr.face;
+  const f3 n0 = ld3(P.vnorm + 4 * (size_t)fs[0]);
+  const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs[1]);
+  const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs[2]);
+  const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
+  if (norm(nn) == 0) return false;
+  return ref_box_test(r, P.refbox + 8 * (size_t)tr.box);
+}
+
+// calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record.
+// CLOSEST: update (t, rank, slot) if 0 <= t < best (rank breaks ties as the reference's order does).
+// ANY:     any valid t >= 0 (shadow(), flyscene.cpp:519).
+template <bool ANY>
+__device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, uint32_t slot, const Ray& r,
+                                         bool active, Hit& h, bool& found) {
+  const f3 n{tr.nx, tr.ny, tr.nz};
+  const float dn = dot(n, r.d);                 // facenormal.dot(dir)
+  const float orth = tr.dist - dot(r.o, n);     // distancePlane - origin.dot(facenormal)
+  const float t = orth / dn;                    // / dir.dot(facenormal)  (same bits as dn)
+  bool cand;
+  if (ANY) cand = active && dn != 0.0f && t >= 0.0f;
+  else cand = active && dn != 0.0f && t >= 0.0f && t < INFINITY && (t < h.t || (t == h.t && tr.rank < h.rank));
+  if (!ballot(cand)) return;
+  const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
+  const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
+  const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
+  const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
+  cand = cand && !(dot(n, a0) < 0 || dot(n, a1) < 0 || dot(n, a2) < 0);
+  if (!ballot(cand)) return;
+  if (cand) {
+    if (accept_candidate(P, tr, e0, e2, a0, a1, a2, r)) {
+      if (ANY) {
+        found = true;
+      } else {
+        h.t = t;
+        h.rank = tr.rank;
+        h.slot = slot;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Wave-packet traversal. STACK_LDS selects the wave stack home: LDS (one uint32 row per wave) or the
+// 64 lanes of one VGPR (v_writelane / v_readlane with an SGPR lane index).
+// ------------------------------------------------------------------------------------------------
+struct WaveStack {
+  uint32_t v = 0;
+  int sp = 0;
+};
+
+template <bool ANY, bool STATS, bool STACK_LDS>
+__device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found, uint32_t* lds_stack,
+                         uint32_t* cnt) {
+  if (P.n_nodes == 0) return;
+  WaveStack st;
+  uint64_t flagstack = 0;  // STATS: per-lane "my ray wanted this entry" bit per stack level
+  bool want = active;      // STATS: this lane's ray intersects the current node
+  uint32_t node = P.root;
+  const float tmax_any = INFINITY;
+  for (;;) {
+    if (!is_leaf(node)) {
+      const Node64 nd = sload_node(P.nodes, node);
+      if (STATS) {
+        if (want) cnt[ST_NODE]++;
+        cnt[ST_WNODE]++;
+      }
+      const float tcut = ANY ? tmax_any : h.t;
+      bool h0, h1;
+      const float t0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut, h0);
+      const float t1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut, h1);
+      h0 = h0 && active;
+      h1 = h1 && active;
+      const uint64_t m0 = ballot(h0), m1 = ballot(h1);
+      if (m0 && m1) {
+        const uint64_t v0 = ballot(h0 && (!h1 || t0 <= t1));
+        const uint64_t v1 = ballot(h1 && (!h0 || t1 < t0));
+        const bool first0 = __popcll(v0) >= __popcll(v1);
+        const uint32_t far = first0 ? nd.child1 : nd.child0;
+        node = first0 ? nd.child0 : nd.child1;
+        if (STACK_LDS) lds_stack[st.sp] = far;
+        else st.v = (lane_id() == st.sp) ? far : st.v;  // v_cmp + v_cndmask: lane sp holds the entry
+        if (STATS) {
+          const bool wf = first0 ? h1 : h0;
+          flagstack = (flagstack & ~(1ull << st.sp)) | ((uint64_t)wf << st.sp);
+          want = first0 ? h0 : h1;
+        }
+        st.sp++;
+      } else if (m0 | m1) {
+        node = m0 ? nd.child0 : nd.child1;
+        if (STATS) want = m0 ? h0 : h1;
+      } else {
+        if (st.sp == 0) break;
+        st.sp--;
+        node = STACK_LDS ? uniform(lds_stack[st.sp]) : (uint32_t)__builtin_amdgcn_readlane(st.v, st.sp);
+        if (STATS) want = (flagstack >> st.sp) & 1;
+      }
+      continue;
+    }
+    // leaf: test its triangles against every lane
+    const uint32_t first = leaf_first(node), count = leaf_count(node);
+    if (STATS) {
+      if (want) cnt[ST_TRI] += count;
+      cnt[ST_WTRI] += count;
+    }
+    for (uint32_t k = 0; k < count; k++) {
+      const TriRec64 tr = sload_tri(P.tris, first + k);
+      test_tri<ANY>(P, tr, first + k, r, active, h, found);
+    }
+    if (ANY) {
+      active = active && !found;
+      if (!ballot(active)) break;
+    }
+    if (st.sp == 0) break;
+    st.sp--;
+    node = STACK_LDS ? uniform(lds_stack[st.sp]) : (uint32_t)__builtin_amdgcn_readlane(st.v, st.sp);
+    if (STATS) want = (flagstack >> st.sp) & 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Shading
+// ------------------------------------------------------------------------------------------------
+struct MatState {  // Flyscene members ka/kd/ks/shininess (flyscene.hpp:179-182)
+  f3 ka, kd, ks;
+  float ns;
+};
+
+__device__ __forceinline__ MatState load_mat(const DevMat& m) {
+  return MatState{f3{m.ka[0], m.ka[1], m.ka[2]}, f3{m.kd[0], m.kd[1], m.kd[2]}, f3{m.ks[0], m.ks[1], m.ks[2]}, m.ns};
+}
+
+// interpolateNormal (flyscene.cpp:572-600) for the hit triangle of this lane (per-lane gathers)
+__device__ __forceinline__ f3 hit_normal(const DevScene& P, const TriRec64& tr, f3 p, int32_t& mat) {
+  const f3 n{tr.nx, tr.ny, tr.nz};
+  const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
+  const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
+  const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
+  const uint4 fs = *reinterpret_cast<const uint4*>(P.fshade + 4 * (size_t)tr.face);
+  mat = (int32_t)fs.w;
+  if (dot(n, a0) < 0 || dot(n, a1) < 0 || dot(n, a2) < 0) return f3{0.0f, 0.0f, 0.0f};
+  const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
+  const float area = norm(cross(e0, neg(e2))) / 2;
+  const float4 n0 = *reinterpret_cast<const float4*>(P.vnorm + 4 * (size_t)fs.x);
+  const float4 n1 = *reinterpret_cast<const float4*>(P.vnorm + 4 * (size_t)fs.y);
+  const float4 n2 = *reinterpret_cast<const float4*>(P.vnorm + 4 * (size_t)fs.z);
+  return blend_normal(f3{n0.x, n0.y, n0.z}, f3{n1.x, n1.y, n1.z}, f3{n2.x, n2.y, n2.z}, area0, area1, area2, area);
+}
+
+__device__ __forceinline__ TriRec64 vload_tri(const TriRec64* base, uint32_t i) {
+  const float4* p = reinterpret_cast<const float4*>(base + i);
+  TriRec64 r;
+  float4* q = reinterpret_cast<float4*>(&r);
+  q[0] = p[0]; q[1] = p[1]; q[2] = p[2]; q[3] = p[3];
+  return r;
+}
+
+// std::pow(float,float) -> powf: evaluated in fp64 then rounded (matches a correctly rounded powf)
+__device__ __forceinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }
+
+// Hit information of one lane, gathered once and reused by every light of calculateColor
+struct HitInfo {
+  f3 p, n;
+  int32_t mat;
+  uint32_t face;
+};
+
+// calcSingleColor body after the shadow test (flyscene.cpp:546-565)
+__device__ __forceinline__ f3 phong(const FrameParams& P, MatState& st, const HitInfo& hi, f3 o, f3 L, const float* I) {
+  if (hi.mat != -1) st = load_mat(P.sc.mats[hi.mat]);
+  const f3 R = phong_r(L, hi.n);
+  const f3 E = normalized(sub(o, hi.p));
+  const float dif = smax(dot(L, hi.n), 0.0f);
+  const float spe = smax(pow_ref(dot(R, E), st.ns), 0.0f);
+  return f3{(I[0] * st.ka.x + (I[0] * st.kd.x) * dif) + (I[0] * st.ks.x) * spe,
+            (I[1] * st.ka.y + (I[1] * st.kd.y) * dif) + (I[1] * st.ks.y) * spe,
+            (I[2] * st.ka.z + (I[2] * st.kd.z) * dif) + (I[2] * st.ks.z) * spe};
+}
+
+__device__ __forceinline__ float clamp01(float x) { return smax(smin(x, 1.0f), 0.0f); }
+
+// calculateColor (flyscene.cpp:603-614). SHADOWS: per light, a wave-packet any-hit traversal from
+// P + 0.003 L (box predicate from P) decides whether the light contributes (calcSingleColor :543).
+template <bool SHADOWS, bool STATS, bool STACK_LDS>
+__device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, const HitInfo& hi, f3 o, bool lane_hit,
+                         uint32_t* lds_stack, uint32_t* cnt) {
+  f3 sum{0.0f, 0.0f, 0.0f};
+  for (int l = 0; l < P.n_lights; l++) {
+    const float* lp = P.lights[l].p;
+    const f3 L = neg(normalized(sub(hi.p, f3{lp[0], lp[1], lp[2]})));
+    bool blocked = false;
+    if (SHADOWS) {
+      Ray sr;
+      sr.o = offset(hi.p, L, 0.003f);
+      sr.d = L;
+      sr.o2 = affv3(P.Minv, hi.p);
+      sr.d2 = normalized(m3v3(P.MS, L));
+      setup_cull(sr);
+      Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      if (STATS && lane_hit) cnt[ST_TOTAL]++;
+      traverse<true, STATS, STACK_LDS>(P.sc, sr, lane_hit, hh, blocked, lds_stack, cnt);
+    }
+    f3 c{0.0f, 0.0f, 0.0f};
+    if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
+    sum = f3{sum.x + c.x, sum.y + c.y, sum.z + c.z};
+  }
+  return f3{clamp01(sum.x), clamp01(sum.y), clamp01(sum.z)};
+}
+
+// ------------------------------------------------------------------------------------------------
+// Render kernel: one wave per 8x8 tile of this shard
+// ------------------------------------------------------------------------------------------------
+template <int MODE, bool STATS, bool HITS, bool STACK_LDS>
+__global__ __launch_bounds__(256) void k_render(FrameParams P) {
+  __shared__ uint32_t lds_stacks[STACK_LDS ? 4 : 1][64];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int wave = (int)uniform(blockIdx.x * 4 + wv);
+  if (wave >= P.n_tiles_shard) return;
+  uint32_t* lds_stack = lds_stacks[STACK_LDS ? wv : 0];
+  const int tile = P.shard_index + wave * P.shard_count;
+  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
+  const bool active = px < P.W && py < P.H;
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+
+  // traceRayThread: o = getCenter(), d = normalize(screenToWorld(i, j) - o)   (flyscene.cpp:301-308)
+  Ray r;
+  {
+    const float nx = (float)(2.0 * (double)((float)px - P.vp[0]) / (double)P.vp[2] - 1.0);
+    const float ny = (float)(1.0 - 2.0 * (double)((float)py - P.vp[1]) / (double)P.vp[3]);
+    const f3 w = affv3(P.vinv, f3{nx * P.xscale, ny * P.yscale, -1.0f});
+    r.o = f3{P.eye[0], P.eye[1], P.eye[2]};
+    r.d = normalized(sub(w, r.o));
+    r.o2 = f3{P.eye_obj[0], P.eye_obj[1], P.eye_obj[2]};
+    r.d2 = normalized(m3v3(P.MS, r.d));
+    setup_cull(r);
+  }
+  if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
+
+  // calculateMinimumFace (flyscene.cpp:373-396)
+  Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  bool dummy = false;
+  traverse<false, STATS, STACK_LDS>(P.sc, r, active, h, dummy, lds_stack, cnt);
+  const bool hit0 = active && h.t != INFINITY;
+  if (STATS && hit0) cnt[ST_HITS]++;
+
+  MatState st = load_mat(P.defmat);
+  HitInfo hi0;
+  TriRec64 tr0;
+  hi0.mat = -1;
+  hi0.face = 0xFFFFFFFFu;
+  hi0.p = f3{0.0f, 0.0f, 0.0f};
+  hi0.n = f3{0.0f, 0.0f, 0.0f};
+  if (hit0) {
+    tr0 = vload_tri(P.sc.tris, h.slot);
+    hi0.face = tr0.face;
+    hi0.p = f3{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
+    hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
+  }
+  constexpr bool FULL = MODE == RT_MODE_FULL;
+  const f3 direct0 = calc_color<FULL, STATS, STACK_LDS>(P, st, hi0, r.o, hit0, lds_stack, cnt);
+  if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
+
+  f3 refl{0.0f, 0.0f, 0.0f};  // traceRay(depth+1): 0 at the depth limit (PRIMARY) or on a miss
+  if (FULL) {
+    // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
+    Ray rr;
+    rr.d = reflect(normalized(r.d), hi0.n);
+    rr.o = offset(hi0.p, rr.d, 0.001f);
+    rr.o2 = affv3(P.Minv, rr.o);
+    rr.d2 = normalized(m3v3(P.MS, rr.d));
+    setup_cull(rr);
+    if (STATS && hit0) cnt[ST_TOTAL]++;
+    Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    traverse<false, STATS, STACK_LDS>(P.sc, rr, hit0, h1, dummy, lds_stack, cnt);
+    const bool hit1 = hit0 && h1.t != INFINITY;
+    HitInfo hi1;
+    hi1.mat = -1;
+    hi1.p = f3{0.0f, 0.0f, 0.0f};
+    hi1.n = f3{0.0f, 0.0f, 0.0f};
+    if (hit1) {
+      const TriRec64 tr1 = vload_tri(P.sc.tris, h1.slot);
+      hi1.face = tr1.face;
+      hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
+      hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
+    }
+    const f3 direct1 = calc_color<true, STATS, STACK_LDS>(P, st, hi1, rr.o, hit1, lds_stack, cnt);
+    if (hit1) {
+      if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
+      // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
+      refl = f3{clamp01(direct1.x + 0.0f * st.ks.x), clamp01(direct1.y + 0.0f * st.ks.y),
+                clamp01(direct1.z + 0.0f * st.ks.z)};
+    }
+  }
+  f3 col;
+  if (hit0) {
+    col = f3{clamp01(direct0.x + refl.x * st.ks.x), clamp01(direct0.y + refl.y * st.ks.y),
+             clamp01(direct0.z + refl.z * st.ks.z)};
+  } else {
+    col = f3{P.bg[0], P.bg[1], P.bg[2]};
+  }
+  if (active) {
+    const size_t pix = (size_t)py * P.W + px;
+    P.rgb[3 * pix + 0] = col.x;
+    P.rgb[3 * pix + 1] = col.y;
+    P.rgb[3 * pix + 2] = col.z;
+    if (HITS) {
+      P.face_out[pix] = hit0 ? (int32_t)hi0.face : -1;
+      P.t_out[pix] = active ? h.t : INFINITY;
+    }
+  }
+  if (STATS) {
+#pragma unroll
+    for (int c = 0; c < ST_COUNT; c++) {
+      unsigned long long v = cnt[c];
+      if (c == ST_WNODE || c == ST_WTRI) v = (lane == 0) ? v : 0;  // wave fetches counted once
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0 && v) atomicAdd(P.stats + c, v);
+    }
+  }
+}
+
+// Ray-list kernels (rt_trace_closest / rt_trace_shadow), 64 rays per wave
+template <bool ANY>
+__global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
+  __shared__ uint32_t lds_stacks[4][64];
+  const int lane = threadIdx.x & 63;
+  const int base = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * 64);
+  if (base >= R.n) return;
+  const int i = base + lane;
+  const bool active = i < R.n;
+  const int j = active ? i : base;
+  Ray r;
+  if (ANY) {  // shadow(P, L): triangle tests from P + 0.003 L, box tests from P (flyscene.cpp:512-519)
+    const f3 p = ld3(R.o + 3 * (size_t)j), L = ld3(R.d + 3 * (size_t)j);
+    r.o = offset(p, L, 0.003f);
+    r.d = L;
+    r.o2 = affv3(P.Minv, p);
+  } else {
+    r.o = ld3(R.o + 3 * (size_t)j);
+    r.d = ld3(R.d + 3 * (size_t)j);
+    r.o2 = affv3(P.Minv, r.o);
+  }
+  r.d2 = normalized(m3v3(P.MS, r.d));
+  setup_cull(r);
+  Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  bool found = false;
+  traverse<ANY, false, false>(P.sc, r, active, h, found, lds_stacks[threadIdx.x >> 6], nullptr);
+  if (!active) return;
+  if (ANY) {
+    R.blocked[i] = found ? 1 : 0;
+  } else if (h.t != INFINITY) {
+    const TriRec64 tr = vload_tri(P.sc.tris, h.slot);
+    R.face[i] = (int32_t)tr.face;
+    R.t[i] = h.t;
+    if (R.P) {
+      R.P[3 * (size_t)i + 0] = r.o.x + h.t * r.d.x;
+      R.P[3 * (size_t)i + 1] = r.o.y + h.t * r.d.y;
+      R.P[3 * (size_t)i + 2] = r.o.z + h.t * r.d.z;
+    }
+  } else {
+    R.face[i] = -1;
+    R.t[i] = INFINITY;
+    if (R.P) R.P[3 * (size_t)i] = R.P[3 * (size_t)i + 1] = R.P[3 * (size_t)i + 2] = 0.0f;
+  }
+}
+
+__global__ void k_debug_math(int op, int n, int in_len, int out_len, const float* in, float* out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) debug_math_case(op, in + (size_t)k * in_len, out + (size_t)k * out_len);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host glue
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+static int dalloc_copy(T** dst, const void* src, size_t bytes, int64_t& total) {
+  *dst = nullptr;
+  if (bytes == 0) bytes = 16;
+  HIPCHECK(hipMalloc((void**)dst, bytes));
+  total += (int64_t)bytes;
+  if (src) HIPCHECK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+int device_upload(rt_scene* s) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device available (the library has no CPU fallback)");
+    return RT_ERR_NO_DEVICE;
+  }
+  int dev = s->opts.device;
+  if (dev < 0) HIPCHECK(hipGetDevice(&dev));
+  if (dev >= ndev) { set_error("device %d out of range (%d devices)", dev, ndev); return RT_ERR_INVALID; }
+  HIPCHECK(hipSetDevice(dev));
+  s->device = dev;
+  hipStream_t st;
+  HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  s->stream = st;
+  HostScene& hs = s->hs;
+  int64_t& tot = s->device_bytes;
+  tot = 0;
+  int rc;
+  if ((rc = dalloc_copy(&s->d_nodes, hs.nodes.data(), hs.nodes.size() * sizeof(Node64), tot))) return rc;
+  if ((rc = dalloc_copy(&s->d_tris, hs.tris.data(), hs.tris.size() * sizeof(TriRec64), tot))) return rc;
+  std::vector<uint32_t> fshade(4 * (size_t)hs.nf);
+  for (int32_t f = 0; f < hs.nf; f++) {
+    fshade[4 * f + 0] = hs.fidx[3 * f + 0];
+    fshade[4 * f + 1] = hs.fidx[3 * f + 1];
+    fshade[4 * f + 2] = hs.fidx[3 * f + 2];
+    fshade[4 * f + 3] = (uint32_t)hs.fmat[f];
+  }
+  if ((rc = dalloc_copy(&s->d_fshade, fshade.data(), fshade.size() * 4, tot))) return rc;
+  std::vector<float> vn(4 * (size_t)hs.nv);
+  for (int32_t i = 0; i < hs.nv; i++) {
+    vn[4 * i] = hs.vnn[i].x; vn[4 * i + 1] = hs.vnn[i].y; vn[4 * i + 2] = hs.vnn[i].z; vn[4 * i + 3] = 0.0f;
+  }
+  if ((rc = dalloc_copy(&s->d_vnorm, vn.data(), vn.size() * 4, tot))) return rc;
+  std::vector<float> rb(8 * hs.boxes.size());
+  for (size_t b = 0; b < hs.boxes.size(); b++) {
+    for (int k = 0; k < 3; k++) { rb[8 * b + k] = hs.boxes[b].low[k]; rb[8 * b + 4 + k] = hs.boxes[b].high[k]; }
+  }
+  if ((rc = dalloc_copy(&s->d_refbox, rb.data(), rb.size() * 4, tot))) return rc;
+  std::vector<DevMat> dm(hs.mats.size());
+  for (size_t m = 0; m < hs.mats.size(); m++) {
+    DevMat& d = dm[m];
+    memset(&d, 0, sizeof d);
+    for (int k = 0; k < 3; k++) { d.ka[k] = hs.mats[m].ka[k]; d.kd[k] = hs.mats[m].kd[k]; d.ks[k] = hs.mats[m].ks[k]; }
+    d.ns = hs.mats[m].shininess;
+  }
+  if ((rc = dalloc_copy(&s->d_mats, dm.data(), dm.size() * sizeof(DevMat), tot))) return rc;
+  if ((rc = dalloc_copy(&s->d_stats, nullptr, 8 * sizeof(unsigned long long), tot))) return rc;
+  return RT_OK;
+}
+
+void device_release(rt_scene* s) {
+  if (s->device == RT_DEVICE_NONE) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
+  void* bufs[] = {s->d_nodes, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats,
+                  s->d_rgb, s->d_face, s->d_t};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
+  s->ev_pool.clear();
+  if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
+  s->stream = nullptr;
+}
+
+static void fill_scene_params(const rt_scene* s, FrameParams& P) {
+  memset(&P, 0, sizeof P);
+  const HostScene& hs = s->hs;
+  P.sc.nodes = s->d_nodes;
+  P.sc.tris = s->d_tris;
+  P.sc.fshade = s->d_fshade;
+  P.sc.vnorm = s->d_vnorm;
+  P.sc.refbox = s->d_refbox;
+  P.sc.mats = s->d_mats;
+  P.sc.root = hs.root;
+  P.sc.n_nodes = (int32_t)hs.nodes.size();
+  memcpy(P.Minv, hs.Minv, 64);
+  memcpy(P.MS, hs.MS, 36);
+  const rt_material& dm = s->opts.default_material;
+  for (int k = 0; k < 3; k++) { P.defmat.ka[k] = dm.ka[k]; P.defmat.kd[k] = dm.kd[k]; P.defmat.ks[k] = dm.ks[k]; }
+  P.defmat.ns = dm.shininess;
+  memcpy(P.bg, s->opts.background, 12);
+}
+
+static int ensure_fb(rt_scene* s, size_t npix) {
+  if (npix <= s->fb_pixels) return RT_OK;
+  if (s->d_rgb) (void)hipFree(s->d_rgb);
+  if (s->d_face) (void)hipFree(s->d_face);
+  if (s->d_t) (void)hipFree(s->d_t);
+  s->d_rgb = nullptr; s->d_face = nullptr; s->d_t = nullptr;
+  HIPCHECK(hipMalloc((void**)&s->d_rgb, npix * 12));
+  HIPCHECK(hipMalloc((void**)&s->d_face, npix * 4));
+  HIPCHECK(hipMalloc((void**)&s->d_t, npix * 4));
+  s->fb_pixels = npix;
+  return RT_OK;
+}
+
+template <int MODE, bool STATS, bool HITS>
+static void launch_render(const FrameParams& P, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_render<MODE, STATS, HITS, false>), dim3(grid), dim3(256), 0, st, P);
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+static int check_device_scene(rt_scene* s) {
+  if (!s) { set_error("null scene"); return RT_ERR_INVALID; }
+  if (s->device == RT_DEVICE_NONE) { set_error("scene was created host-only (RT_DEVICE_NONE)"); return RT_ERR_NO_DEVICE; }
+  HIPCHECK(hipSetDevice(s->device));
+  return RT_OK;
+}
+
+extern "C" int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
+                               const rt_frame* fr) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  if (!cam || !fr || fr->width <= 0 || fr->height <= 0 || n_lights < 0 || n_lights > RT_MAX_LIGHTS ||
+      (n_lights && !lights)) {
+    set_error("rt_render: invalid arguments");
+    return RT_ERR_INVALID;
+  }
+  if (fr->mode != RT_MODE_PRIMARY && fr->mode != RT_MODE_FULL) { set_error("rt_render: bad mode %d", fr->mode); return RT_ERR_INVALID; }
+  const int sc = fr->shard_count > 0 ? fr->shard_count : 1;
+  const int si = fr->shard_index;
+  if (si < 0 || si >= sc) { set_error("rt_render: shard %d of %d", si, sc); return RT_ERR_INVALID; }
+  const size_t npix = (size_t)fr->width * fr->height;
+  if ((rc = ensure_fb(s, npix))) return rc;
+  FrameParams P;
+  fill_scene_params(s, P);
+  // camera (camera.hpp:115-118,155-173,263-266)
+  affinv(cam->view_matrix, P.vinv);
+  {
+    float L[9], Li[9];
+    linear_of(cam->view_matrix, L);
+    m3inv(L, Li);
+    const f3 e = m3v3(Li, f3{-cam->view_matrix[12], -cam->view_matrix[13], -cam->view_matrix[14]});
+    P.eye[0] = e.x; P.eye[1] = e.y; P.eye[2] = e.z;
+    const f3 eo = affv3(s->hs.Minv, e);
+    P.eye_obj[0] = eo.x; P.eye_obj[1] = eo.y; P.eye_obj[2] = eo.z;
+  }
+  memcpy(P.vp, cam->viewport, 16);
+  const float persp = (float)((double)1.0f / tan((double)(cam->fovy / 2.0f) * (M_PI / 180.0)));
+  const float scale = (float)(1.0 / (double)persp);
+  P.xscale = cam->aspect_ratio * scale;
+  P.yscale = scale;
+  P.n_lights = n_lights;
+  for (int l = 0; l < n_lights; l++) {
+    memcpy(P.lights[l].p, lights[l].position, 12);
+    memcpy(P.lights[l].c, lights[l].color, 12);
+  }
+  P.W = fr->width;
+  P.H = fr->height;
+  P.tiles_x = (fr->width + 7) / 8;
+  P.tiles_y = (fr->height + 7) / 8;
+  const int ntiles = P.tiles_x * P.tiles_y;
+  P.shard_index = si;
+  P.shard_count = sc;
+  P.n_tiles_shard = ntiles > si ? (ntiles - si + sc - 1) / sc : 0;
+  P.mode = fr->mode;
+  P.flags = fr->flags;
+  P.rgb = s->d_rgb;
+  P.face_out = s->d_face;
+  P.t_out = s->d_t;
+  P.stats = s->d_stats;
+  hipStream_t st = (hipStream_t)s->stream;
+  const bool stats = (fr->flags & RT_FRAME_STATS) != 0;
+  const bool hits = (fr->flags & RT_FRAME_WRITE_HITS) != 0;
+  if (stats) HIPCHECK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st));
+  const int grid = (P.n_tiles_shard + 3) / 4;
+  if (s->ev_used + 2 > s->ev_pool.size()) {
+    if (s->ev_pool.size() >= 4096) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }
+    for (int k = 0; k < 2; k++) {
+      hipEvent_t e;
+      HIPCHECK(hipEventCreate(&e));
+      s->ev_pool.push_back(e);
+    }
+  }
+  hipEvent_t ev_a = (hipEvent_t)s->ev_pool[s->ev_used], ev_b = (hipEvent_t)s->ev_pool[s->ev_used + 1];
+  s->ev_used += 2;
+  HIPCHECK(hipEventRecord(ev_a, st));
+  if (grid > 0) {
+    if (fr->mode == RT_MODE_PRIMARY) {
+      if (stats) { if (hits) launch_render<RT_MODE_PRIMARY, true, true>(P, grid, st); else launch_render<RT_MODE_PRIMARY, true, false>(P, grid, st); }
+      else { if (hits) launch_render<RT_MODE_PRIMARY, false, true>(P, grid, st); else launch_render<RT_MODE_PRIMARY, false, false>(P, grid, st); }
+    } else {
+      if (stats) { if (hits) launch_render<RT_MODE_FULL, true, true>(P, grid, st); else launch_render<RT_MODE_FULL, true, false>(P, grid, st); }
+      else { if (hits) launch_render<RT_MODE_FULL, false, true>(P, grid, st); else launch_render<RT_MODE_FULL, false, false>(P, grid, st); }
+    }
+    HIPCHECK(hipGetLastError());
+  }
+  HIPCHECK(hipEventRecord(ev_b, st));
+  s->last_W = fr->width;
+  s->last_H = fr->height;
+  s->last_flags = fr->flags;
+  // primary rays of this shard: pixels inside the frame of the shard's tiles
+  int64_t rays = 0;
+  for (int t = si; t < ntiles; t += sc) {
+    const int tx = t % P.tiles_x, ty = t / P.tiles_x;
+    rays += (int64_t)std::min(8, fr->width - tx * 8) * std::min(8, fr->height - ty * 8);
+  }
+  s->last_rays = rays;
+  s->pending = true;
+  return RT_OK;
+}
+
+extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  HIPCHECK(hipStreamSynchronize((hipStream_t)s->stream));
+  struct Reset { rt_scene* s; ~Reset() { s->ev_used = 0; s->pending = false; } } reset_{s};
+  if (out) {
+    memset(out, 0, sizeof *out);
+    double tot = 0.0;
+    for (size_t k = 0; k + 1 < s->ev_used; k += 2) {
+      float ms = 0.0f;
+      HIPCHECK(hipEventElapsedTime(&ms, (hipEvent_t)s->ev_pool[k], (hipEvent_t)s->ev_pool[k + 1]));
+      tot += ms;
+    }
+    out->kernel_ms = tot;
+    out->launches = (int64_t)(s->ev_used / 2);
+    out->primary_rays = s->last_rays;
+    out->total_rays = s->last_rays;
+    if (s->last_flags & RT_FRAME_STATS) {
+      unsigned long long c[8];
+      HIPCHECK(hipMemcpy(c, s->d_stats, sizeof c, hipMemcpyDeviceToHost));
+      out->node_visits = (int64_t)c[ST_NODE];
+      out->tri_tests = (int64_t)c[ST_TRI];
+      out->wave_node_fetches = (int64_t)c[ST_WNODE];
+      out->wave_tri_fetches = (int64_t)c[ST_WTRI];
+      out->hits = (int64_t)c[ST_HITS];
+      out->total_rays = (int64_t)c[ST_TOTAL];
+    }
+  }
+  return RT_OK;
+}
+
+extern "C" int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  HIPCHECK(hipStreamSynchronize((hipStream_t)s->stream));
+  const size_t npix = (size_t)s->last_W * s->last_H;
+  if (rgb) HIPCHECK(hipMemcpy(rgb, s->d_rgb, npix * 12, hipMemcpyDeviceToHost));
+  if ((face || t) && !(s->last_flags & RT_FRAME_WRITE_HITS)) { set_error("last frame was rendered without RT_FRAME_WRITE_HITS"); return RT_ERR_INVALID; }
+  if (face) HIPCHECK(hipMemcpy(face, s->d_face, npix * 4, hipMemcpyDeviceToHost));
+  if (t) HIPCHECK(hipMemcpy(t, s->d_t, npix * 4, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights, const rt_frame* fr,
+                         float* out_rgb, rt_stats* stats) {
+  int rc = rt_render_async(s, cam, lights, n_lights, fr);
+  if (rc) return rc;
+  if ((rc = rt_synchronize(s, stats))) return rc;
+  if (!out_rgb) return RT_OK;
+  const int W = fr->width, H = fr->height;
+  const int sc = fr->shard_count > 0 ? fr->shard_count : 1;
+  if (sc == 1) return rt_frame_download(s, out_rgb, nullptr, nullptr);
+  std::vector<float> full((size_t)W * H * 3);
+  if ((rc = rt_frame_download(s, full.data(), nullptr, nullptr))) return rc;
+  const int tiles_x = (W + 7) / 8, ntiles = tiles_x * ((H + 7) / 8);
+  for (int t = fr->shard_index; t < ntiles; t += sc) {
+    const int tx = t % tiles_x, ty = t / tiles_x;
+    for (int y = ty * 8; y < std::min(H, ty * 8 + 8); y++) {
+      const size_t o = ((size_t)y * W + tx * 8) * 3;
+      memcpy(out_rgb + o, full.data() + o, sizeof(float) * 3 * (size_t)(std::min(W, tx * 8 + 8) - tx * 8));
+    }
+  }
+  return RT_OK;
+}
+
+static int trace_rays(rt_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t, float* P3,
+                      int32_t* blocked, bool any) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  if (n < 0 || (n && (!o || !d))) { set_error("trace: invalid arguments"); return RT_ERR_INVALID; }
+  if (n == 0) return RT_OK;
+  FrameParams P;
+  fill_scene_params(s, P);
+  float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr, *d_P = nullptr;
+  int32_t *d_face = nullptr, *d_bl = nullptr;
+  const size_t n3 = (size_t)n * 12;
+  hipStream_t st = (hipStream_t)s->stream;
+  HIPCHECK(hipMalloc((void**)&d_o, n3));
+  HIPCHECK(hipMalloc((void**)&d_d, n3));
+  HIPCHECK(hipMemcpy(d_o, o, n3, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(d_d, d, n3, hipMemcpyHostToDevice));
+  RayParams R{d_o, d_d, n, nullptr, nullptr, nullptr, nullptr};
+  if (any) {
+    HIPCHECK(hipMalloc((void**)&d_bl, (size_t)n * 4));
+    R.blocked = d_bl;
+  } else {
+    HIPCHECK(hipMalloc((void**)&d_face, (size_t)n * 4));
+    HIPCHECK(hipMalloc((void**)&d_t, (size_t)n * 4));
+    R.face = d_face;
+    R.t = d_t;
+    if (P3) { HIPCHECK(hipMalloc((void**)&d_P, n3)); R.P = d_P; }
+  }
+  const int grid = (n + 255) / 256;
+  if (any) hipLaunchKernelGGL(k_rays<true>, dim3(grid), dim3(256), 0, st, P, R);
+  else hipLaunchKernelGGL(k_rays<false>, dim3(grid), dim3(256), 0, st, P, R);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));
+  if (any) {
+    HIPCHECK(hipMemcpy(blocked, d_bl, (size_t)n * 4, hipMemcpyDeviceToHost));
+  } else {
+    if (face) HIPCHECK(hipMemcpy(face, d_face, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (t) HIPCHECK(hipMemcpy(t, d_t, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (P3) HIPCHECK(hipMemcpy(P3, d_P, n3, hipMemcpyDeviceToHost));
+  }
+  for (void* b : {(void*)d_o, (void*)d_d, (void*)d_t, (void*)d_P, (void*)d_face, (void*)d_bl})
+    if (b) (void)hipFree(b);
+  return RT_OK;
+}
+
+extern "C" int rt_trace_closest(rt_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t,
+                                float* P3) {
+  return trace_rays(s, n, o, d, face, t, P3, nullptr, false);
+}
+
+extern "C" int rt_trace_shadow(rt_scene* s, int32_t n, const float* P3, const float* L3, int32_t* blocked) {
+  if (!blocked && n > 0) { set_error("rt_trace_shadow: null output"); return RT_ERR_INVALID; }
+  return trace_rays(s, n, P3, L3, nullptr, nullptr, nullptr, blocked, true);
+}
+
+extern "C" int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out) {
+  static const int in_len[] = {6, 3, 6, 12, 19, 20, 9, 16, 4, 6, 6, 6, 6, 13, 3, 16, 24};
+  static const int out_len[] = {1, 3, 3, 3, 3, 4, 9, 16, 16, 3, 3, 3, 3, 3, 1, 3, 3};
+  if (op < 0 || op > 16 || n <= 0 || !in || !out) { set_error("rt_debug_math_device: bad arguments"); return RT_ERR_INVALID; }
+  if (rt_device_count() == 0) { set_error("no HIP device"); return RT_ERR_NO_DEVICE; }
+  float *di = nullptr, *dout = nullptr;
+  const size_t ib = (size_t)n * in_len[op] * 4, ob = (size_t)n * out_len[op] * 4;
+  HIPCHECK(hipMalloc((void**)&di, ib));
+  HIPCHECK(hipMalloc((void**)&dout, ob));
+  HIPCHECK(hipMemcpy(di, in, ib, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_debug_math, dim3((n + 255) / 256), dim3(256), 0, 0, (int)op, (int)n, in_len[op], out_len[op], di, dout);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipDeviceSynchronize());
+  HIPCHECK(hipMemcpy(out, dout, ob, hipMemcpyDeviceToHost));
+  (void)hipFree(di);
+  (void)hipFree(dout);
+  return RT_OK;
+}

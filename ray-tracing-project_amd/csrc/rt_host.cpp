@@ -1,0 +1,859 @@
+// rt_host.cpp -- host side of the MI355X ray-traversal library: Tucano-semantics scene ingest, the
+// reference's flat box partition (which defines closest-hit tie-breaking and the per-face box
+// predicate), the traversal BVH build, camera setup, PPM output and the host-only C ABI entry points.
+//
+// Reference semantics restated here (file:line in plindhorst/Ray-Tracing-Project):
+//   OBJ/MTL ingest      tucano/utils/objimporter.hpp:81-351, tucano/utils/mtlIO.hpp:36-140
+//   normalisation       tucano/mesh.hpp:592-628, tucano/model.hpp:102-105,169-173
+//   face normals        tucano/mesh.hpp:448-482
+//   flat box partition  src/BoundingBox.cpp:41-161, src/flyscene.cpp:399-428
+//   camera              tucano/camera.hpp:115-118,155-173,263-266; tucano/utils/flycamera.hpp:76-202
+//   PPM writer          tucano/utils/ppmIO.hpp:135-156
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <future>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rt_scene.h"
+
+using rt::f3;
+
+namespace rt {
+static thread_local std::string g_err;
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+}  // namespace rt
+
+extern "C" const char* rt_last_error(void) { return rt::g_err.c_str(); }
+extern "C" int rt_version(void) { return RT_API_VERSION; }
+
+// =====================================================================================================
+// Ingest (Tucano::MeshImporter semantics)
+// =====================================================================================================
+namespace {
+
+void mtl_default(rt_material& m) {  // Tucano::Material::Mtl defaults (materials/mtl.hpp:22-40)
+  for (int k = 0; k < 3; k++) { m.ka[k] = 0.3f; m.kd[k] = 0.5f; m.ks[k] = 1.0f; }
+  m.shininess = 10.0f;
+  m.optical_density = 0.0f;
+  m.dissolve = 1.0f;
+}
+
+std::string path_name(const std::string& s) {  // getPathName (mtlIO.hpp:36-40)
+  size_t found = s.find_last_of("/\\");
+  return s.substr(0, found + 1);
+}
+
+void erase_crlf(std::string& s) {
+  s.erase(std::remove(s.begin(), s.end(), '\n'), s.end());
+  s.erase(std::remove(s.begin(), s.end(), '\r'), s.end());
+}
+
+// MaterialImporter::loadMTL (mtlIO.hpp:49-140): tokens split on single spaces, atof values
+bool load_mtl(rt_mesh* m, const std::string& filename) {
+  std::ifstream in(filename.c_str(), std::ios::in);
+  if (!in) return false;
+  for (std::string line; std::getline(in, line);) {
+    std::stringstream ss(line);
+    if (ss.str().empty()) continue;
+    std::string s;
+    std::vector<std::string> tok;
+    while (std::getline(ss, s, ' ')) tok.push_back(s);
+    if (tok.empty() || tok[0] == "#") continue;
+    if (tok[0] == "newmtl") {
+      rt_material mt;
+      mtl_default(mt);
+      m->mats.push_back(mt);
+      std::string nm = tok.size() > 1 ? tok[1] : std::string();
+      erase_crlf(nm);
+      m->mat_names.push_back(nm);
+      continue;
+    }
+    if (m->mats.empty()) continue;  // reference: materials.back() on an empty vector (UB); ignored
+    rt_material& cur = m->mats.back();
+    auto f = [&](size_t i) { return i < tok.size() ? (float)atof(tok[i].c_str()) : 0.0f; };
+    if (tok[0] == "Ns") cur.shininess = f(1);
+    else if (tok[0] == "Ka") { cur.ka[0] = f(1); cur.ka[1] = f(2); cur.ka[2] = f(3); }
+    else if (tok[0] == "Kd") { cur.kd[0] = f(1); cur.kd[1] = f(2); cur.kd[2] = f(3); }
+    else if (tok[0] == "Ks") { cur.ks[0] = f(1); cur.ks[1] = f(2); cur.ks[2] = f(3); }
+    else if (tok[0] == "Ni") cur.optical_density = f(1);
+    else if (tok[0] == "d") cur.dissolve = f(1);
+  }
+  if (m->mats.empty()) {  // "if no mtllib then just create a default material"
+    rt_material mt;
+    mtl_default(mt);
+    m->mats.push_back(mt);
+    m->mat_names.push_back("");
+  }
+  return true;
+}
+
+// istringstream >> float for the numeric tokens of v/vn lines (num_get -> strtof on the prefix)
+int parse_floats(const char* s, const char* end, float* out, int n) {
+  for (int k = 0; k < n; k++) {
+    while (s < end && (*s == ' ' || *s == '\t' || *s == '\r' || *s == '\v' || *s == '\f')) s++;
+    if (s >= end) return k;
+    char* e;
+    out[k] = strtof(s, &e);
+    if (e == s) return k;
+    s = e;
+  }
+  return n;
+}
+
+// Mesh::loadVertices bounding box / scale / centre (mesh.hpp:592-628); std::max/min argument order
+void load_vertices(rt_mesh* m) {
+  size_t nv = m->v4.size() / 4;
+  m->scale = 1.0f;
+  m->center[0] = m->center[1] = m->center[2] = 0.0f;
+  if (nv == 0) return;
+  const float* v = m->v4.data();
+  float xMax = v[0], xMin = v[0], yMax = v[1], yMin = v[1], zMax = v[2], zMin = v[2];
+  for (size_t i = 0; i < nv; i++) {
+    const float* p = v + 4 * i;
+    xMax = rt::smax(p[0], xMax); yMax = rt::smax(p[1], yMax); zMax = rt::smax(p[2], zMax);
+    xMin = rt::smin(p[0], xMin); yMin = rt::smin(p[1], yMin); zMin = rt::smin(p[2], zMin);
+  }
+  float ext = rt::smax(rt::smax(std::fabs(xMax - xMin), std::fabs(yMax - yMin)), std::fabs(zMax - zMin));
+  m->scale = (float)(1.0 / (double)ext);
+  m->center[0] = (float)((double)(xMax + xMin) / 2.0);
+  m->center[1] = (float)((double)(yMax + yMin) / 2.0);
+  m->center[2] = (float)((double)(zMax + zMin) / 2.0);
+}
+
+// computeNormals (objimporter.hpp:81-106)
+void compute_normals(rt_mesh* m, const std::vector<std::vector<uint32_t>>& groups) {
+  size_t nv = m->v4.size() / 4;
+  m->vn3.assign(3 * nv, 0.0f);
+  auto V = [&](uint32_t i) { return f3{m->v4[4 * i], m->v4[4 * i + 1], m->v4[4 * i + 2]}; };
+  for (const auto& g : groups)
+    for (size_t i = 0; i + 2 < g.size(); i += 3) {
+      f3 v0 = rt::normalized(rt::sub(V(g[i + 1]), V(g[i])));
+      f3 v1 = rt::normalized(rt::sub(V(g[i + 2]), V(g[i])));
+      f3 n = rt::normalized(rt::cross(v0, v1));
+      for (int k = 0; k < 3; k++) {
+        float* d = &m->vn3[3 * g[i + k]];
+        d[0] = d[0] + n.x; d[1] = d[1] + n.y; d[2] = d[2] + n.z;
+      }
+    }
+  for (size_t i = 0; i < nv; i++) {
+    f3 n = rt::normalized(f3{m->vn3[3 * i], m->vn3[3 * i + 1], m->vn3[3 * i + 2]});
+    m->vn3[3 * i] = n.x; m->vn3[3 * i + 1] = n.y; m->vn3[3 * i + 2] = n.z;
+  }
+}
+
+// createFaces (mesh.hpp:448-482), normalizeModelMatrix + getShapeModelMatrix (model.hpp)
+int finish_mesh(rt_mesh* m, const std::vector<std::vector<uint32_t>>& groups, const std::vector<int32_t>& gmat,
+                bool have_vn) {
+  const size_t nv = m->v4.size() / 4;
+  load_vertices(m);
+  if (!have_vn) compute_normals(m, groups);
+  m->fidx.clear(); m->fn3.clear(); m->fmat.clear();
+  auto V = [&](uint32_t i) { return f3{m->v4[4 * i], m->v4[4 * i + 1], m->v4[4 * i + 2]}; };
+  if (nv > 0)
+    for (size_t g = 0; g < groups.size(); g++) {
+      const auto& ix = groups[g];
+      if (ix.size() % 3 != 0) {
+        rt::set_error("index group of %zu indices is not a multiple of 3 (reference reads out of bounds)", ix.size());
+        return RT_ERR_INVALID;
+      }
+      for (size_t i = 0; i < ix.size(); i += 3) {
+        for (int k = 0; k < 3; k++) {
+          if (ix[i + k] >= nv) { rt::set_error("face vertex index %u out of range", ix[i + k] + 1); return RT_ERR_INVALID; }
+          m->fidx.push_back(ix[i + k]);
+        }
+        m->fmat.push_back(gmat[g]);
+        f3 v1 = rt::normalized(rt::sub(V(ix[i + 2]), V(ix[i])));
+        f3 v0 = rt::normalized(rt::sub(V(ix[i + 1]), V(ix[i])));
+        f3 n = rt::normalized(rt::cross(v0, v1));
+        m->fn3.push_back(n.x); m->fn3.push_back(n.y); m->fn3.push_back(n.z);
+      }
+    }
+  float shape[16], model[16];
+  rt::identity4(shape);
+  rt::scale4(shape, m->scale);
+  rt::translate4(shape, f3{-m->center[0], -m->center[1], -m->center[2]});
+  rt::identity4(model);
+  rt::affmul(model, shape, m->M);
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" int rt_mesh_load_obj(const char* path, rt_mesh** out) {
+  if (!path || !out) { rt::set_error("rt_mesh_load_obj: null argument"); return RT_ERR_INVALID; }
+  *out = nullptr;
+  FILE* f = fopen(path, "rb");
+  if (!f) { rt::set_error("Cannot open %s", path); return RT_ERR_IO; }
+  std::string buf;
+  fseek(f, 0, SEEK_END);
+  long len = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  buf.resize(len > 0 ? (size_t)len : 0);
+  if (len > 0 && fread(&buf[0], 1, (size_t)len, f) != (size_t)len) { fclose(f); rt::set_error("read error %s", path); return RT_ERR_IO; }
+  fclose(f);
+
+  auto m = new rt_mesh();
+  const std::string dir = path_name(path);
+  std::vector<std::vector<uint32_t>> groups(1);
+  std::vector<int32_t> gmat(1, -1);
+  std::vector<float> norms;
+  int32_t current_mat = -1;
+  size_t pos = 0;
+  while (pos < buf.size()) {  // std::getline(in, line)
+    size_t nl = buf.find('\n', pos);
+    if (nl == std::string::npos) nl = buf.size();
+    const char* ls = buf.data() + pos;
+    const char* le = buf.data() + nl;
+    size_t L = nl - pos;
+    pos = nl + 1;
+    if (L >= 6 && !strncmp(ls, "mtllib", 6)) {
+      if (L < 7) { delete m; rt::set_error("malformed mtllib line"); return RT_ERR_INVALID; }
+      std::string fn = dir + std::string(ls + 7, le);
+      erase_crlf(fn);
+      load_mtl(m, fn);
+    } else if (L >= 6 && !strncmp(ls, "usemtl", 6)) {
+      if (!groups.back().empty()) { groups.emplace_back(); gmat.push_back(-1); }
+      if (L < 7) { delete m; rt::set_error("malformed usemtl line"); return RT_ERR_INVALID; }
+      std::string nm(ls + 7, le);
+      erase_crlf(nm);
+      for (size_t i = 0; i < m->mat_names.size(); i++)
+        if (m->mat_names[i] == nm) current_mat = (int32_t)i;
+      gmat.back() = current_mat;
+    } else if (L >= 2 && ls[0] == 'v' && ls[1] == ' ') {
+      float v[3] = {0, 0, 0};
+      parse_floats(ls + 2, le, v, 3);
+      m->v4.insert(m->v4.end(), {v[0], v[1], v[2], 1.0f});
+    } else if (L >= 2 && ls[0] == 'v' && ls[1] == 'n') {
+      float n[3] = {0, 0, 0};
+      if (L >= 3) parse_floats(ls + 3, le, n, 3);
+      norms.insert(norms.end(), {n[0], n[1], n[2]});
+    } else if (L >= 2 && ls[0] == 'f' && ls[1] == ' ') {
+      const char* p = ls + 2;
+      while (p < le) {
+        while (p < le && (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\v' || *p == '\f')) p++;
+        if (p >= le) break;
+        const char* e = p;
+        while (e < le && !(*e == ' ' || *e == '\t' || *e == '\r' || *e == '\v' || *e == '\f')) e++;
+        long vid = strtol(std::string(p, e).c_str(), nullptr, 10);  // stoi(element before '/')
+        groups.back().push_back((uint32_t)(vid - 1));
+        p = e;
+      }
+    }
+  }
+  const size_t nv = m->v4.size() / 4;
+  const bool have_vn = norms.size() == 3 * nv;
+  if (have_vn) m->vn3 = norms;
+  // only non-empty index groups become index buffers (objimporter.hpp:312-319)
+  std::vector<std::vector<uint32_t>> g2;
+  std::vector<int32_t> m2;
+  for (size_t g = 0; g < groups.size(); g++)
+    if (!groups[g].empty()) { g2.push_back(std::move(groups[g])); m2.push_back(gmat[g]); }
+  int rc = finish_mesh(m, g2, m2, have_vn);
+  if (rc) { delete m; return rc; }
+  *out = m;
+  return RT_OK;
+}
+
+extern "C" int rt_mesh_from_arrays(int32_t nv, const float* v3, const float* vn3, int32_t ng, const int32_t* gcount,
+                                   const uint32_t* idx, const int32_t* gmat, int32_t nm, const rt_material* mats,
+                                   rt_mesh** out) {
+  if (!out || nv < 0 || ng < 0 || (nv && !v3) || (ng && (!gcount || !gmat))) {
+    rt::set_error("rt_mesh_from_arrays: invalid arguments");
+    return RT_ERR_INVALID;
+  }
+  *out = nullptr;
+  auto m = new rt_mesh();
+  m->v4.resize(4 * (size_t)nv);
+  for (int32_t i = 0; i < nv; i++) {
+    m->v4[4 * i] = v3[3 * i]; m->v4[4 * i + 1] = v3[3 * i + 1]; m->v4[4 * i + 2] = v3[3 * i + 2]; m->v4[4 * i + 3] = 1.0f;
+  }
+  if (vn3) m->vn3.assign(vn3, vn3 + 3 * (size_t)nv);
+  for (int32_t i = 0; i < nm; i++) { m->mats.push_back(mats[i]); m->mat_names.push_back("material_" + std::to_string(i)); }
+  std::vector<std::vector<uint32_t>> groups(ng);
+  std::vector<int32_t> gm(ng);
+  size_t off = 0;
+  for (int32_t g = 0; g < ng; g++) {
+    if (gcount[g] < 0) { delete m; rt::set_error("negative group size"); return RT_ERR_INVALID; }
+    groups[g].assign(idx + off, idx + off + gcount[g]);
+    gm[g] = gmat[g];
+    if (gm[g] >= nm) { delete m; rt::set_error("group material %d out of range", gm[g]); return RT_ERR_INVALID; }
+    off += (size_t)gcount[g];
+  }
+  int rc = finish_mesh(m, groups, gm, vn3 != nullptr);
+  if (rc) { delete m; return rc; }
+  *out = m;
+  return RT_OK;
+}
+
+extern "C" void rt_mesh_destroy(rt_mesh* m) { delete m; }
+
+extern "C" int rt_mesh_get_desc(const rt_mesh* m, rt_mesh_desc* d) {
+  if (!m || !d) { rt::set_error("rt_mesh_get_desc: null argument"); return RT_ERR_INVALID; }
+  d->n_vertices = (int32_t)(m->v4.size() / 4);
+  d->vertices = m->v4.data();
+  d->vertex_normals = m->vn3.data();
+  d->n_faces = (int32_t)m->fmat.size();
+  d->face_vertex_ids = m->fidx.data();
+  d->face_normals = m->fn3.data();
+  d->face_material_ids = m->fmat.data();
+  d->n_materials = (int32_t)m->mats.size();
+  d->materials = m->mats.data();
+  memcpy(d->shape_model_matrix, m->M, 64);
+  return RT_OK;
+}
+
+// =====================================================================================================
+// Synthetic soup, PPM, camera
+// =====================================================================================================
+static inline uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static inline float u01(uint64_t& s) { return (float)(splitmix64(s) >> 40) * (1.0f / 16777216.0f); }
+
+extern "C" void rt_generate_soup(int32_t n, uint64_t seed, float* v) {
+  uint64_t s = seed;
+  for (int32_t t = 0; t < n; t++) {
+    float c[3];
+    for (int k = 0; k < 3; k++) c[k] = u01(s) - 0.5f;
+    for (int j = 0; j < 3; j++)
+      for (int k = 0; k < 3; k++) {
+        float off = (u01(s) * 2.0f - 1.0f) * 0.01f;
+        v[9 * (size_t)t + 3 * j + k] = c[k] + off;
+      }
+  }
+}
+
+// (int)(255*c) with x86 cvttss2si semantics for out-of-range / NaN (0x80000000)
+static inline int to_int_x86(float x) {
+  if (!(x >= -2147483648.0f && x < 2147483648.0f)) return INT_MIN;
+  return (int)x;
+}
+
+extern "C" int rt_write_ppm(const char* path, const float* rgb, int32_t W, int32_t H) {
+  if (!path || !rgb || W <= 0 || H <= 0) { rt::set_error("rt_write_ppm: invalid arguments"); return RT_ERR_INVALID; }
+  FILE* f = fopen(path, "wb");
+  if (!f) { rt::set_error("cannot write %s", path); return RT_ERR_IO; }
+  std::string out;
+  out.reserve((size_t)W * H * 12 + 64);
+  out += "P3\n" + std::to_string(W) + " " + std::to_string(H) + "\n255\n";
+  char tmp[64];
+  for (int32_t j = 0; j < H; j++) {
+    for (int32_t i = 0; i < W; i++) {
+      const float* c = rgb + 3 * ((size_t)j * W + i);
+      int n = snprintf(tmp, sizeof tmp, "%d %d %d ", std::min(255, to_int_x86(255 * c[0])),
+                       std::min(255, to_int_x86(255 * c[1])), std::min(255, to_int_x86(255 * c[2])));
+      out.append(tmp, (size_t)n);
+    }
+    out += "\n";
+  }
+  size_t wr = fwrite(out.data(), 1, out.size(), f);
+  fclose(f);
+  if (wr != out.size()) { rt::set_error("short write %s", path); return RT_ERR_IO; }
+  return RT_OK;
+}
+
+extern "C" void rt_camera_flycam(int32_t W, int32_t H, float dx, float dy, float dz, rt_camera* c) {
+  // Flycamera::translate (flycamera.hpp:196-202), yaw = identity at rotation_Y_axis = 0
+  const float I9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  const float speed = 0.05f;  // flycamera.hpp:107
+  f3 yv = rt::m3v3(I9, f3{-dx, -dy, dz});
+  f3 tv{0.0f + yv.x * speed, 0.0f + yv.y * speed, 0.0f + yv.z * speed};
+  // updateViewMatrix (flycamera.hpp:166-191) at zero rotation
+  rt::identity4(c->view_matrix);
+  rt::translate4(c->view_matrix, f3{0.0f, 0.0f, -2.0f});
+  rt::translate4(c->view_matrix, tv);
+  c->viewport[0] = 0.0f; c->viewport[1] = 0.0f; c->viewport[2] = (float)W; c->viewport[3] = (float)H;
+  c->fovy = 60.0f;                     // flyscene.cpp:14
+  c->aspect_ratio = (float)W / (float)H;
+}
+
+extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
+  memset(o, 0, sizeof *o);
+  o->device = -1;
+  o->min_faces = 300;       // flyscene.hpp:168
+  o->max_boxes = INT32_MAX; // flyscene.hpp:169
+  o->leaf_size = 0;
+  for (int k = 0; k < 3; k++) { o->default_material.ka[k] = 0.2f; o->background[k] = 0.9f; }
+  o->default_material.kd[0] = 0.9f; o->default_material.kd[1] = 0.9f; o->default_material.kd[2] = 0.0f;
+  o->default_material.shininess = 0.0f;
+  o->default_material.dissolve = 0.0f;
+}
+
+// =====================================================================================================
+// Reference flat box partition (BoundingBox.cpp / flyscene.cpp:399-428)
+// =====================================================================================================
+namespace rt {
+namespace {
+struct BoxBuilder {
+  const float* v4;
+  const uint32_t* f;
+  std::vector<RefBox>& boxes;
+  const float* V(int32_t face, int k) const { return v4 + 4 * (size_t)f[3 * (size_t)face + k]; }
+
+  static void reshape(RefBox& b) { for (int k = 0; k < 3; k++) b.shape[k] = b.high[k] - b.low[k]; }
+
+  bool has_face(const RefBox& b, int32_t face) const {  // hasFace / hasVertex (inclusive)
+    for (int k = 0; k < 3; k++) {
+      const float* v = V(face, k);
+      if (!(v[0] >= b.low[0] && v[0] <= b.high[0] && v[1] >= b.low[1] && v[1] <= b.high[1] &&
+            v[2] >= b.low[2] && v[2] <= b.high[2]))
+        return false;
+    }
+    return true;
+  }
+  void fit(RefBox& b) const {  // fitFaces: first-vertex init, if/else-if min/max
+    if (b.faces.empty()) return;
+    const float* t = V(b.faces[0], 0);
+    float mn[3] = {t[0], t[1], t[2]}, mx[3] = {t[0], t[1], t[2]};
+    for (int32_t face : b.faces)
+      for (int j = 0; j < 3; j++) {
+        const float* v = V(face, j);
+        for (int a = 0; a < 3; a++) {
+          if (v[a] < mn[a]) mn[a] = v[a];
+          else if (v[a] > mx[a]) mx[a] = v[a];
+        }
+      }
+    for (int a = 0; a < 3; a++) { b.low[a] = mn[a]; b.high[a] = mx[a]; }
+    reshape(b);
+  }
+  float average(const RefBox& b, int axis) const {  // averageVertexCoord: sequential float sum
+    float avg = 0.0f;
+    for (int32_t face : b.faces) {
+      avg += V(face, 0)[axis];
+      avg += V(face, 1)[axis];
+      avg += V(face, 2)[axis];
+    }
+    avg /= (float)(b.faces.size() * 3);
+    return avg;
+  }
+  // splitBox: 1 = split into a new box, 0 = axis failed (returned `this`), -1 = nullptr
+  int split(size_t bi) {
+    RefBox& b = boxes[bi];
+    float oldLow[3], oldHigh[3];
+    memcpy(oldLow, b.low, 12);
+    memcpy(oldHigh, b.high, 12);
+    const float w = b.shape[0], h = b.shape[1], d = b.shape[2];
+    int choice;
+    if ((w >= h || b.failed[1]) && (w >= d || b.failed[2]) && !b.failed[0]) choice = 0;
+    else if ((h >= w || b.failed[0]) && (h >= d || b.failed[2]) && !b.failed[1]) choice = 1;
+    else if (!(b.failed[0] && b.failed[1] && b.failed[2])) choice = 2;
+    else return -1;
+    b.high[choice] = average(b, choice);
+    reshape(b);
+    std::vector<int32_t> inside, outside;  // outsideFaces: stable partition
+    inside.reserve(b.faces.size());
+    for (int32_t face : b.faces) (has_face(b, face) ? inside : outside).push_back(face);
+    if (inside.empty() || outside.empty()) {
+      b.faces = inside.empty() ? std::move(outside) : std::move(inside);
+      b.failed[choice] = true;
+      memcpy(b.low, oldLow, 12);
+      memcpy(b.high, oldHigh, 12);
+      reshape(b);
+      return 0;
+    }
+    b.faces = std::move(inside);
+    b.failed[0] = b.failed[1] = b.failed[2] = false;
+    RefBox nb;
+    nb.faces = std::move(outside);
+    boxes.push_back(std::move(nb));  // invalidates b
+    fit(boxes.back());
+    fit(boxes[bi]);
+    return 1;
+  }
+};
+}  // namespace
+
+void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes) {
+  hs.boxes.clear();
+  BoxBuilder bb{v4, hs.fidx.data(), hs.boxes};
+  RefBox b0;
+  b0.faces.resize(hs.nf);
+  for (int32_t i = 0; i < hs.nf; i++) b0.faces[i] = i;
+  hs.boxes.push_back(std::move(b0));
+  bb.fit(hs.boxes[0]);
+  bool notDone = true;
+  while (notDone && (int64_t)hs.boxes.size() < (int64_t)max_boxes) {
+    notDone = false;
+    const size_t ncur = hs.boxes.size();
+    for (size_t bi = 0; bi < ncur; bi++) {
+      RefBox& b = hs.boxes[bi];
+      if ((int64_t)b.faces.size() > min_faces && (!b.failed[0] || !b.failed[1] || !b.failed[2])) {
+        int r = bb.split(bi);
+        while (r == 0) r = bb.split(bi);
+        notDone = true;
+      }
+    }
+  }
+  hs.face_rank.assign(hs.nf, 0);
+  hs.face_box.assign(hs.nf, 0);
+  uint32_t rank = 0;
+  for (size_t bi = 0; bi < hs.boxes.size(); bi++)
+    for (int32_t face : hs.boxes[bi].faces) {
+      hs.face_rank[face] = rank++;
+      hs.face_box[face] = (uint32_t)bi;
+    }
+}
+
+// =====================================================================================================
+// Traversal BVH: binned SAH BVH2 over world-space triangle bounds, 64-byte nodes in DFS order.
+// Child boxes are padded outward so node culling is conservative with respect to the reference's
+// (rounded) triangle test: a triangle the reference accepts is never behind a culled box.
+// =====================================================================================================
+namespace {
+struct Prim { float lo[3], hi[3], c[3]; };
+struct Aabb {
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const float* l, const float* h) {
+    for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], l[k]); hi[k] = std::max(hi[k], h[k]); }
+  }
+  void growp(const float* p) { grow(p, p); }
+  float area() const {
+    float d[3];
+    for (int k = 0; k < 3; k++) d[k] = std::max(0.0f, hi[k] - lo[k]);
+    return 2.0f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+  }
+};
+
+struct BvhBuilder {
+  const std::vector<Prim>& prims;
+  std::vector<uint32_t>& idx;
+  std::vector<Node64>& nodes;
+  std::atomic<uint32_t> next{0};
+  int leaf_size;
+  float pad;
+  std::atomic<int> max_depth{0}, leaves{0};
+  static constexpr int kBins = 32;
+  static constexpr float kTrav = 1.0f, kIsect = 1.0f;
+
+  void set_child(Node64& n, int which, const Aabb& b, uint32_t h) const {
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; k++) { lo[k] = b.lo[k] - pad; hi[k] = b.hi[k] + pad; }
+    if (which == 0) {
+      n.c0lx = lo[0]; n.c0hx = hi[0]; n.c0ly = lo[1]; n.c0hy = hi[1]; n.c0lz = lo[2]; n.c0hz = hi[2];
+      n.child0 = h;
+    } else {
+      n.c1lx = lo[0]; n.c1hx = hi[0]; n.c1ly = lo[1]; n.c1hy = hi[1]; n.c1lz = lo[2]; n.c1hz = hi[2];
+      n.child1 = h;
+    }
+  }
+
+  // builds [b,e); returns the handle and the (unpadded) bounds of the subtree
+  uint32_t build(uint32_t b, uint32_t e, int depth, Aabb& box) {
+    Aabb cb;
+    box = Aabb();
+    for (uint32_t i = b; i < e; i++) { box.grow(prims[idx[i]].lo, prims[idx[i]].hi); cb.growp(prims[idx[i]].c); }
+    const uint32_t n = e - b;
+    int md = max_depth.load();
+    while (depth > md && !max_depth.compare_exchange_weak(md, depth)) {}
+    auto make_leaf_h = [&]() { leaves++; return make_leaf(b, n); };
+    if (n == 1) return make_leaf_h();
+    // choose split
+    int axis = -1;
+    uint32_t mid = b;
+    float best_cost = INFINITY;
+    float ext[3];
+    for (int k = 0; k < 3; k++) ext[k] = cb.hi[k] - cb.lo[k];
+    const bool force_median = depth >= kMaxDepth - 20;
+    if (!force_median) {
+      int best_bin = -1;
+      for (int k = 0; k < 3; k++) {
+        if (!(ext[k] > 0.0f)) continue;
+        Aabb bins[kBins];
+        uint32_t cnt[kBins] = {0};
+        const float sc = kBins / ext[k];
+        for (uint32_t i = b; i < e; i++) {
+          const Prim& p = prims[idx[i]];
+          int bi = std::min(kBins - 1, (int)((p.c[k] - cb.lo[k]) * sc));
+          bins[bi].grow(p.lo, p.hi);
+          cnt[bi]++;
+        }
+        float right_area[kBins];
+        uint32_t right_cnt[kBins];
+        Aabb acc;
+        uint32_t c = 0;
+        for (int i = kBins - 1; i > 0; i--) {
+          acc.grow(bins[i].lo, bins[i].hi);
+          c += cnt[i];
+          right_area[i] = acc.area();
+          right_cnt[i] = c;
+        }
+        Aabb lacc;
+        uint32_t lc = 0;
+        for (int i = 0; i < kBins - 1; i++) {
+          lacc.grow(bins[i].lo, bins[i].hi);
+          lc += cnt[i];
+          if (lc == 0 || right_cnt[i + 1] == 0) continue;
+          float cost = lacc.area() * lc + right_area[i + 1] * right_cnt[i + 1];
+          if (cost < best_cost) { best_cost = cost; axis = k; best_bin = i; }
+        }
+      }
+      const float parent_area = std::max(box.area(), 1e-30f);
+      const float split_cost = kTrav + kIsect * best_cost / parent_area;
+      if ((int)n <= leaf_size && (axis < 0 || (float)n * kIsect <= split_cost)) return make_leaf_h();
+      if (axis >= 0) {
+        const float sc = kBins / ext[axis];
+        const float lo = cb.lo[axis];
+        auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t pi) {
+          return std::min(kBins - 1, (int)((prims[pi].c[axis] - lo) * sc)) <= best_bin;
+        });
+        mid = (uint32_t)(it - idx.begin());
+      }
+    } else if ((int)n <= leaf_size) {
+      return make_leaf_h();
+    }
+    if (axis < 0 || mid == b || mid == e) {
+      // degenerate centroids or forced: object median along the widest centroid axis
+      if ((int)n <= kMaxLeaf && !(ext[0] > 0 || ext[1] > 0 || ext[2] > 0)) return make_leaf_h();
+      int k = (ext[0] >= ext[1] && ext[0] >= ext[2]) ? 0 : (ext[1] >= ext[2] ? 1 : 2);
+      mid = b + n / 2;
+      std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e,
+                       [&](uint32_t x, uint32_t y) { return prims[x].c[k] < prims[y].c[k]; });
+    }
+    const uint32_t me = next.fetch_add(1);
+    Aabb lb, rb;
+    uint32_t lh, rh;
+    if (n > 65536 && depth < 4) {
+      auto fut = std::async(std::launch::async, [&]() { return build(b, mid, depth + 1, lb); });
+      rh = build(mid, e, depth + 1, rb);
+      lh = fut.get();
+    } else {
+      lh = build(b, mid, depth + 1, lb);
+      rh = build(mid, e, depth + 1, rb);
+    }
+    Node64 nd{};
+    set_child(nd, 0, lb, lh);
+    set_child(nd, 1, rb, rh);
+    nodes[me] = nd;
+    return me;
+  }
+};
+}  // namespace
+
+void build_bvh(HostScene& hs, int leaf_size) {
+  hs.nodes.clear();
+  hs.tris.clear();
+  hs.depth = 0;
+  hs.leaves = 0;
+  if (hs.nf == 0) { hs.root = 0; return; }
+  std::vector<Prim> prims(hs.nf);
+  Aabb world;
+  for (int32_t f = 0; f < hs.nf; f++) {
+    Prim& p = prims[f];
+    for (int k = 0; k < 3; k++) { p.lo[k] = INFINITY; p.hi[k] = -INFINITY; }
+    for (int j = 0; j < 3; j++) {
+      const f3& w = hs.wv[hs.fidx[3 * f + j]];
+      const float c[3] = {w.x, w.y, w.z};
+      for (int k = 0; k < 3; k++) { p.lo[k] = std::min(p.lo[k], c[k]); p.hi[k] = std::max(p.hi[k], c[k]); }
+    }
+    for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.lo[k] + p.hi[k]);
+    world.grow(p.lo, p.hi);
+  }
+  float ext = 0.0f, mag = 0.0f;
+  for (int k = 0; k < 3; k++) {
+    ext = std::max(ext, world.hi[k] - world.lo[k]);
+    mag = std::max(mag, std::max(std::fabs(world.lo[k]), std::fabs(world.hi[k])));
+  }
+  // conservative padding: covers the reference's rounding of P = o + t d and of the inclusive edge
+  // tests for ray origins within ~16 scene extents (DESIGN.md "Exactness of culling")
+  const float pad = 2e-5f * std::max(std::max(ext, mag), 1e-3f);
+  std::vector<uint32_t> idx(hs.nf);
+  for (int32_t f = 0; f < hs.nf; f++) idx[f] = (uint32_t)f;
+  std::vector<Node64> tmp((size_t)std::max(hs.nf, 1));
+  BvhBuilder B{prims, idx, tmp};
+  B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
+  B.pad = pad;
+  Aabb rootb;
+  uint32_t root = B.build(0, (uint32_t)hs.nf, 0, rootb);
+  uint32_t nn = B.next.load();
+  if (is_leaf(root)) {  // whole scene in one leaf: wrap in a node whose second child never hits
+    Node64 nd{};
+    B.set_child(nd, 0, rootb, root);
+    nd.c1lx = nd.c1ly = nd.c1lz = INFINITY;
+    nd.c1hx = nd.c1hy = nd.c1hz = -INFINITY;
+    nd.child1 = make_leaf(0, 1);
+    tmp[0] = nd;
+    nn = 1;
+    root = 0;
+  }
+  // re-layout interior nodes in depth-first (near child first) order
+  hs.nodes.resize(nn);
+  std::vector<uint32_t> remap(nn, UINT32_MAX), order;
+  order.reserve(nn);
+  std::vector<uint32_t> st{root};
+  while (!st.empty()) {
+    uint32_t n = st.back();
+    st.pop_back();
+    remap[n] = (uint32_t)order.size();
+    order.push_back(n);
+    const Node64& nd = tmp[n];
+    if (!is_leaf(nd.child1)) st.push_back(nd.child1);
+    if (!is_leaf(nd.child0)) st.push_back(nd.child0);
+  }
+  for (uint32_t i = 0; i < nn; i++) {
+    Node64 nd = tmp[order[i]];
+    if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
+    if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
+    hs.nodes[i] = nd;
+  }
+  hs.root = 0;
+  hs.depth = B.max_depth.load() + 1;
+  hs.leaves = B.leaves.load();
+  // triangle records in leaf order
+  hs.tris.resize(hs.nf);
+  for (int32_t s = 0; s < hs.nf; s++) {
+    const uint32_t f = idx[s];
+    TriRec64& r = hs.tris[s];
+    const f3& n = hs.fnn[f];
+    const f3& w0 = hs.wv[hs.fidx[3 * f]];
+    const f3& w1 = hs.wv[hs.fidx[3 * f + 1]];
+    const f3& w2 = hs.wv[hs.fidx[3 * f + 2]];
+    r.nx = n.x; r.ny = n.y; r.nz = n.z; r.dist = hs.fdist[f];
+    r.w0x = w0.x; r.w0y = w0.y; r.w0z = w0.z;
+    r.w1x = w1.x; r.w1y = w1.y; r.w1z = w1.z;
+    r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
+    r.rank = hs.face_rank[f];
+    r.face = f;
+    r.box = hs.face_box[f];
+  }
+}
+
+}  // namespace rt
+
+// =====================================================================================================
+// Scene creation (host preparation + device upload)
+// =====================================================================================================
+extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts, rt_scene** out) {
+  if (!d || !out) { rt::set_error("rt_scene_create: null argument"); return RT_ERR_INVALID; }
+  *out = nullptr;
+  if (d->n_vertices < 0 || d->n_faces < 0 || (d->n_faces && (!d->face_vertex_ids || !d->face_normals || !d->face_material_ids)) ||
+      (d->n_vertices && (!d->vertices || !d->vertex_normals))) {
+    rt::set_error("rt_scene_create: invalid mesh description");
+    return RT_ERR_INVALID;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  auto s = new rt_scene();
+  if (opts) s->opts = *opts; else rt_scene_opts_default(&s->opts);
+  if (s->opts.min_faces <= 0) s->opts.min_faces = 300;
+  if (s->opts.max_boxes <= 0) s->opts.max_boxes = INT32_MAX;
+  const int leaf = s->opts.leaf_size > 0 ? s->opts.leaf_size : 4;
+  rt::HostScene& hs = s->hs;
+  hs.nv = d->n_vertices;
+  hs.nf = d->n_faces;
+  memcpy(hs.M, d->shape_model_matrix, 64);
+  rt::affinv(hs.M, hs.Minv);
+  rt::linear_of(hs.Minv, hs.MS);
+  hs.fidx.assign(d->face_vertex_ids, d->face_vertex_ids + 3 * (size_t)hs.nf);
+  hs.fmat.assign(d->face_material_ids, d->face_material_ids + hs.nf);
+  hs.mats.assign(d->materials, d->materials + d->n_materials);
+  for (int32_t f = 0; f < hs.nf; f++) {
+    for (int k = 0; k < 3; k++)
+      if (hs.fidx[3 * f + k] >= (uint32_t)hs.nv) {
+        delete s;
+        rt::set_error("face %d references vertex %u of %d", f, hs.fidx[3 * f + k], hs.nv);
+        return RT_ERR_INVALID;
+      }
+    if (hs.fmat[f] >= d->n_materials || hs.fmat[f] < -1) {
+      delete s;
+      rt::set_error("face %d has material id %d (n_materials %d)", f, hs.fmat[f], d->n_materials);
+      return RT_ERR_INVALID;
+    }
+  }
+  // hoisted per-vertex / per-face invariants (same expressions as flyscene.cpp:449-450,459,574-577,599)
+  hs.wv.resize(hs.nv);
+  hs.vnn.resize(hs.nv);
+  for (int32_t i = 0; i < hs.nv; i++) {
+    const float* v = d->vertices + 4 * (size_t)i;
+    hs.wv[i] = rt::affv3(hs.M, f3{v[0] / v[3], v[1] / v[3], v[2] / v[3]});
+    const float* n = d->vertex_normals + 3 * (size_t)i;
+    hs.vnn[i] = rt::normalized(f3{n[0], n[1], n[2]});
+  }
+  hs.fnn.resize(hs.nf);
+  hs.fdist.resize(hs.nf);
+  for (int32_t f = 0; f < hs.nf; f++) {
+    const float* n = d->face_normals + 3 * (size_t)f;
+    hs.fnn[f] = rt::normalized(f3{n[0], n[1], n[2]});
+    hs.fdist[f] = rt::dot(hs.fnn[f], hs.wv[hs.fidx[3 * f]]);
+  }
+  rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
+  rt::build_bvh(hs, leaf);
+  if (hs.depth > rt::kMaxDepth + 2) {  // the wave stack holds 64 entries
+    delete s;
+    rt::set_error("BVH depth %d exceeds the traversal stack", hs.depth);
+    return RT_ERR_UNSUPPORTED;
+  }
+  s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (s->opts.device != RT_DEVICE_NONE) {
+    int rc = rt::device_upload(s);
+    if (rc) { delete s; return rc; }
+  }
+  *out = s;
+  return RT_OK;
+}
+
+extern "C" void rt_scene_destroy(rt_scene* s) {
+  if (!s) return;
+  rt::device_release(s);
+  delete s;
+}
+
+extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
+  if (!s || !o) { rt::set_error("rt_scene_get_info: null argument"); return RT_ERR_INVALID; }
+  o->n_faces = s->hs.nf;
+  o->n_vertices = s->hs.nv;
+  o->n_ref_boxes = (int32_t)s->hs.boxes.size();
+  o->bvh_nodes = (int32_t)s->hs.nodes.size();
+  o->bvh_leaves = s->hs.leaves;
+  o->bvh_depth = s->hs.depth;
+  o->device_bytes = s->device_bytes;
+  o->build_ms = s->build_ms;
+  o->device = s->device;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_ref_boxes(const rt_scene* s, float* bounds6, int32_t* counts, int32_t* face_order) {
+  if (!s) { rt::set_error("rt_scene_ref_boxes: null scene"); return RT_ERR_INVALID; }
+  size_t off = 0;
+  for (size_t i = 0; i < s->hs.boxes.size(); i++) {
+    const rt::RefBox& b = s->hs.boxes[i];
+    if (bounds6) { memcpy(bounds6 + 6 * i, b.low, 12); memcpy(bounds6 + 6 * i + 3, b.high, 12); }
+    if (counts) counts[i] = (int32_t)b.faces.size();
+    if (face_order) memcpy(face_order + off, b.faces.data(), sizeof(int32_t) * b.faces.size());
+    off += b.faces.size();
+  }
+  return RT_OK;
+}
+
+// =====================================================================================================
+// Verification hook: Eigen-order primitives on the host (op codes: oracle/eigen_kat.cpp)
+// =====================================================================================================
+#include "rt_kat.h"
+
+extern "C" int rt_debug_math_host(int32_t op, int32_t n, const float* in, float* out) {
+  static const int in_len[] = {6, 3, 6, 12, 19, 20, 9, 16, 4, 6, 6, 6, 6, 13, 3, 16, 24};
+  static const int out_len[] = {1, 3, 3, 3, 3, 4, 9, 16, 16, 3, 3, 3, 3, 3, 1, 3, 3};
+  if (op < 0 || op > 16 || n < 0 || !in || !out) { rt::set_error("rt_debug_math_host: bad op"); return RT_ERR_INVALID; }
+  for (int32_t k = 0; k < n; k++)
+    if (rt::debug_math_case(op, in + (size_t)k * in_len[op], out + (size_t)k * out_len[op])) return RT_ERR_INVALID;
+  return RT_OK;
+}

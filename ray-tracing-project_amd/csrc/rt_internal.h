@@ -1,0 +1,112 @@
+// rt_internal.h -- shared host/device data layout of the MI355X ray-traversal library.
+//
+// HBM layout (one copy per device; all arrays 16-byte aligned, read-only during a frame):
+//   nodes    Node64[n_nodes]       BVH2 interior nodes: both children's padded AABBs + child handles
+//                                  (one 64-B record = one s_load_dwordx16 per wave per visit)
+//   tris     TriRec64[n_faces]     exact-test data in BVH leaf order: unit face normal, plane distance,
+//                                  world vertices, reference rank / face id / reference box id
+//   fshade   uint4[n_faces]        per face id: vertex ids + material (touched only by the final hit)
+//   vnorm    float4[n_vertices]    normalised vertex normals (interpolateNormal, flyscene.cpp:599)
+//   refbox   float4[2*n_boxes]     reference flat boxes, object space (BoundingBox::low/high)
+//   mats     float4[3*n_mats]      ka|Ns, kd|-, ks|- per material
+// Frame buffers: rgb float[H][W][3]; optional face int32[H][W], t float[H][W]; stats counters.
+#pragma once
+#include <cstdint>
+
+#include "rt_math.h"
+
+namespace rt {
+
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kLeafCountShift = 27;          // 4 bits: count - 1 (1..16 triangles)
+constexpr uint32_t kLeafFirstMask = (1u << 27) - 1;  // first triangle slot (< 134M)
+constexpr int kMaxLeaf = 16;
+constexpr int kMaxDepth = 60;  // wave stack holds 64 entries; occupancy <= depth
+
+RT_HD bool is_leaf(uint32_t h) { return (h & kLeafBit) != 0; }
+RT_HD uint32_t leaf_first(uint32_t h) { return h & kLeafFirstMask; }
+RT_HD uint32_t leaf_count(uint32_t h) { return ((h >> kLeafCountShift) & 15u) + 1u; }
+inline uint32_t make_leaf(uint32_t first, uint32_t count) {
+  return kLeafBit | ((count - 1u) << kLeafCountShift) | first;
+}
+
+struct alignas(16) Node64 {
+  // child 0: lo.x hi.x lo.y hi.y | lo.z hi.z ; child 1: lo.x hi.x | lo.y hi.y lo.z hi.z
+  float c0lx, c0hx, c0ly, c0hy;
+  float c0lz, c0hz, c1lx, c1hx;
+  float c1ly, c1hy, c1lz, c1hz;
+  uint32_t child0, child1, pad0, pad1;
+};
+static_assert(sizeof(Node64) == 64, "node record must be 64 bytes");
+
+struct alignas(16) TriRec64 {
+  float nx, ny, nz, dist;  // face.normal.normalized(), facenormal.dot(vert0)  (flyscene.cpp:450,459)
+  float w0x, w0y, w0z, w1x;
+  float w1y, w1z, w2x, w2y;
+  float w2z;
+  uint32_t rank;  // position in the reference's (box, in-box) iteration order: tie-break key
+  uint32_t face;  // original mesh face index
+  uint32_t box;   // reference box holding the face (intersectBox predicate)
+};
+static_assert(sizeof(TriRec64) == 64, "triangle record must be 64 bytes");
+
+struct alignas(16) DevMat {
+  float ka[3], ns;
+  float kd[3], pad0;
+  float ks[3], pad1;
+};
+
+struct Light {
+  float p[3], c[3];
+};
+
+// Device scene view (pointers stay wave-uniform: SGPRs)
+struct DevScene {
+  const Node64* nodes;
+  const TriRec64* tris;
+  const uint32_t* fshade;  // uint4 per face
+  const float* vnorm;      // float4 per vertex
+  const float* refbox;     // 2 float4 per box
+  const DevMat* mats;
+  uint32_t root;           // root handle; n_nodes == 0 -> empty scene
+  int32_t n_nodes;
+};
+
+// Per-launch parameters (kernel argument, ~1 KB)
+struct FrameParams {
+  DevScene sc;
+  float Minv[16];          // getShapeModelMatrix().inverse()  (flyscene.cpp:486)
+  float MS[9];             // its linear block                  (flyscene.cpp:487)
+  DevMat defmat;           // Flyscene sticky defaults (flyscene.hpp:179-182)
+  float bg[3];
+  // camera (reproduces Camera::screenToWorld, camera.hpp:155-173)
+  float vinv[16];          // view_matrix.inverse()
+  float eye[3];            // getCenter()
+  float eye_obj[3];        // Minv * eye (object-space origin of every primary ray's box test)
+  float vp[4];             // viewport
+  float xscale, yscale;    // aspect_ratio * scale, scale
+  // lights
+  int32_t n_lights;
+  Light lights[16];
+  // frame
+  int32_t W, H, tiles_x, tiles_y;
+  int32_t shard_index, shard_count, n_tiles_shard;
+  int32_t mode, flags;
+  float* rgb;
+  int32_t* face_out;
+  float* t_out;
+  unsigned long long* stats;  // [8] counters (RT_FRAME_STATS)
+};
+
+// Ray-list query parameters (rt_trace_closest / rt_trace_shadow)
+struct RayParams {
+  const float* o;  // [n][3]
+  const float* d;  // [n][3]
+  int32_t n;
+  int32_t* face;
+  float* t;
+  float* P;
+  int32_t* blocked;
+};
+
+}  // namespace rt

@@ -1,0 +1,84 @@
+// rt_scene.h -- internal definitions of rt_mesh / rt_scene (host + device halves).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/rt/rt_api.h"
+#include "rt_internal.h"
+
+struct rt_mesh {
+  std::vector<float> v4;       // [nv][4]
+  std::vector<float> vn3;      // [nv][3]
+  std::vector<uint32_t> fidx;  // [nf][3]
+  std::vector<float> fn3;      // [nf][3]
+  std::vector<int32_t> fmat;   // [nf]
+  std::vector<rt_material> mats;
+  std::vector<std::string> mat_names;
+  float scale = 1.0f, center[3] = {0, 0, 0};
+  float M[16];
+};
+
+namespace rt {
+
+struct RefBox {
+  float low[3], high[3], shape[3];
+  bool failed[3] = {false, false, false};
+  std::vector<int32_t> faces;
+};
+
+struct HostScene {
+  int32_t nv = 0, nf = 0;
+  std::vector<f3> wv;        // world vertices  (M * v)
+  std::vector<f3> vnn;       // normalised vertex normals
+  std::vector<f3> fnn;       // normalised face normals
+  std::vector<float> fdist;  // facenormal.dot(vert0)
+  std::vector<uint32_t> fidx;
+  std::vector<int32_t> fmat;
+  std::vector<rt_material> mats;
+  float M[16], Minv[16], MS[9];
+  std::vector<RefBox> boxes;
+  std::vector<uint32_t> face_rank, face_box;
+  // BVH
+  std::vector<Node64> nodes;
+  std::vector<TriRec64> tris;  // leaf order
+  uint32_t root = 0;
+  int32_t depth = 0, leaves = 0;
+};
+
+void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes);
+void build_bvh(HostScene& hs, int leaf_size);
+void set_error(const char* fmt, ...);
+
+}  // namespace rt
+
+struct rt_scene {
+  rt_scene_opts opts;
+  rt::HostScene hs;
+  double build_ms = 0.0;
+  int32_t device = RT_DEVICE_NONE;
+  // device state (rt_device.hip)
+  void* stream = nullptr;
+  std::vector<void*> ev_pool;   // event pairs, one per render launch since the last synchronize
+  size_t ev_used = 0;
+  rt::Node64* d_nodes = nullptr;
+  rt::TriRec64* d_tris = nullptr;
+  uint32_t* d_fshade = nullptr;
+  float* d_vnorm = nullptr;
+  float* d_refbox = nullptr;
+  rt::DevMat* d_mats = nullptr;
+  unsigned long long* d_stats = nullptr;
+  int64_t device_bytes = 0;
+  // frame buffers (grown on demand)
+  float* d_rgb = nullptr;
+  int32_t* d_face = nullptr;
+  float* d_t = nullptr;
+  size_t fb_pixels = 0;
+  int32_t last_W = 0, last_H = 0, last_flags = 0;
+  int64_t last_rays = 0, last_total_rays = 0;
+  bool pending = false;
+};
+
+namespace rt {
+int device_upload(rt_scene* s);
+void device_release(rt_scene* s);
+}  // namespace rt

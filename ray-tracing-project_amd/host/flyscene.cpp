@@ -1,0 +1,91 @@
+// flyscene.cpp -- see flyscene.hpp. Reference: src/flyscene.cpp:9-64 (initialize), :250-297
+// (raytraceScene); tucano/utils/flycamera.hpp (camera); all hot-path work happens in librtamd.
+#include "flyscene.hpp"
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+
+#include "../csrc/rt_math.h"
+
+namespace fly {
+
+void Flycamera::reset() {
+  tv_[0] = tv_[1] = tv_[2] = 0.0f;
+  updateViewMatrix();
+}
+
+void Flycamera::translate(float dx, float dy, float dz) {
+  const float I9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // AngleAxisf(rotation_Y_axis = 0, UnitY)
+  const rt::f3 yv = rt::m3v3(I9, rt::f3{-dx, -dy, dz});
+  tv_[0] = tv_[0] + yv.x * speed_;
+  tv_[1] = tv_[1] + yv.y * speed_;
+  tv_[2] = tv_[2] + yv.z * speed_;
+}
+
+void Flycamera::updateViewMatrix() {
+  rt::identity4(view_);
+  rt::translate4(view_, rt::f3{0.0f, 0.0f, -2.0f});  // default_translation
+  rt::translate4(view_, rt::f3{tv_[0], tv_[1], tv_[2]});
+}
+
+rt_camera Flycamera::camera() const {
+  rt_camera c;
+  memcpy(c.view_matrix, view_, sizeof view_);
+  memcpy(c.viewport, vp_, sizeof vp_);
+  c.fovy = fovy_;
+  c.aspect_ratio = aspect_;
+  return c;
+}
+
+Flyscene::~Flyscene() {
+  rt_scene_destroy(scene_);
+  rt_mesh_destroy(mesh_);
+}
+
+void Flyscene::initialize(int width, int height, const std::string& obj_path, int device) {
+  flycamera.setPerspectiveMatrix(60.0f, width / (float)height);
+  flycamera.setViewport((float)width, (float)height);
+  flycamera.reset();
+  if (rt_mesh_load_obj(obj_path.c_str(), &mesh_) != RT_OK) {
+    fprintf(stderr, "%s\n", rt_last_error());  // reference: "Cannot open", empty mesh
+    return;
+  }
+  lights.push_back({Vec3{-0.5f, 2.0f, 3.0f}, Vec3{1.0f, 1.0f, 1.0f}});
+  rt_mesh_desc d;
+  rt_mesh_get_desc(mesh_, &d);
+  rt_scene_opts o;
+  rt_scene_opts_default(&o);
+  o.device = device;
+  if (rt_scene_create(&d, &o, &scene_) != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
+}
+
+double Flyscene::raytraceScene(int width, int height) {
+  if (!scene_) { fprintf(stderr, "raytraceScene: no scene\n"); return -1.0; }
+  if (width == 0 || height == 0) {
+    width = flycamera.viewportWidth();
+    height = flycamera.viewportHeight();
+  }
+  flycamera.updateViewMatrix();
+  rt_camera cam = flycamera.camera();
+  std::vector<rt_light> ls(lights.size());
+  for (size_t i = 0; i < lights.size(); i++) {
+    ls[i] = rt_light{{lights[i].first.x, lights[i].first.y, lights[i].first.z},
+                     {lights[i].second.x, lights[i].second.y, lights[i].second.z}};
+  }
+  last_image.assign((size_t)width * height * 3, 0.0f);
+  rt_frame fr{width, height, mode, 0, 1, 0};
+  rt_stats st;
+  printf("ray tracing ...\n");
+  const auto t0 = std::chrono::steady_clock::now();
+  if (rt_render(scene_, &cam, ls.data(), (int32_t)ls.size(), &fr, last_image.data(), &st) != RT_OK) {
+    fprintf(stderr, "%s\n", rt_last_error());
+    return -1.0;
+  }
+  if (rt_write_ppm(output.c_str(), last_image.data(), width, height) != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
+  const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  printf(" ray tracing done! \n\nTime it took to render(in seconds): %.6f (kernel %.3f ms)\n", wall, st.kernel_ms);
+  return st.kernel_ms;
+}
+
+}  // namespace fly

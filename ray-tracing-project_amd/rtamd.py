@@ -1,0 +1,318 @@
+"""ctypes binding of librtamd.so (include/rt/rt_api.h) for tests and bench.py.
+
+Plumbing only: the product is the C ABI + gfx950 kernels. Loading fails loudly if the built library
+is missing (there is no Python or CPU fallback for any render/trace call).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "librtamd.so")
+
+RT_MODE_PRIMARY = 0
+RT_MODE_FULL = 1
+RT_FRAME_WRITE_HITS = 1
+RT_FRAME_STATS = 2
+RT_DEVICE_NONE = -2
+
+# Every symbol include/rt/rt_api.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "rt_mesh_load_obj", "rt_mesh_from_arrays", "rt_mesh_destroy", "rt_mesh_get_desc", "rt_generate_soup",
+    "rt_write_ppm", "rt_scene_opts_default", "rt_scene_create", "rt_scene_destroy", "rt_scene_get_info",
+    "rt_scene_ref_boxes", "rt_camera_flycam", "rt_render", "rt_render_async", "rt_synchronize",
+    "rt_frame_download", "rt_trace_closest", "rt_trace_shadow", "rt_device_count", "rt_version",
+    "rt_last_error", "rt_debug_math_host", "rt_debug_math_device",
+]
+
+
+class Material(C.Structure):
+    _fields_ = [("ka", C.c_float * 3), ("kd", C.c_float * 3), ("ks", C.c_float * 3), ("shininess", C.c_float),
+                ("optical_density", C.c_float), ("dissolve", C.c_float)]
+
+
+class MeshDesc(C.Structure):
+    _fields_ = [("n_vertices", C.c_int32), ("vertices", C.c_void_p), ("vertex_normals", C.c_void_p),
+                ("n_faces", C.c_int32), ("face_vertex_ids", C.c_void_p), ("face_normals", C.c_void_p),
+                ("face_material_ids", C.c_void_p), ("n_materials", C.c_int32), ("materials", C.c_void_p),
+                ("shape_model_matrix", C.c_float * 16)]
+
+
+class SceneOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("min_faces", C.c_int32), ("max_boxes", C.c_int32),
+                ("leaf_size", C.c_int32), ("default_material", Material), ("background", C.c_float * 3)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("n_faces", C.c_int32), ("n_vertices", C.c_int32), ("n_ref_boxes", C.c_int32),
+                ("bvh_nodes", C.c_int32), ("bvh_leaves", C.c_int32), ("bvh_depth", C.c_int32),
+                ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("device", C.c_int32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("view_matrix", C.c_float * 16), ("viewport", C.c_float * 4), ("fovy", C.c_float),
+                ("aspect_ratio", C.c_float)]
+
+
+class Light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("color", C.c_float * 3)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("mode", C.c_int32), ("shard_index", C.c_int32),
+                ("shard_count", C.c_int32), ("flags", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_int64), ("primary_rays", C.c_int64), ("total_rays", C.c_int64),
+                ("hits", C.c_int64), ("node_visits", C.c_int64), ("tri_tests", C.c_int64),
+                ("wave_node_fetches", C.c_int64), ("wave_tri_fetches", C.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"librtamd.so not built: {LIB_PATH} (run `make` or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.rt_last_error.restype = C.c_char_p
+        L.rt_mesh_load_obj.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.rt_mesh_from_arrays.argtypes = [C.c_int32, vp, vp, C.c_int32, vp, vp, vp, C.c_int32, vp, C.POINTER(vp)]
+        L.rt_mesh_destroy.argtypes = [vp]
+        L.rt_mesh_get_desc.argtypes = [vp, C.POINTER(MeshDesc)]
+        L.rt_generate_soup.argtypes = [C.c_int32, C.c_uint64, vp]
+        L.rt_generate_soup.restype = None
+        L.rt_write_ppm.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
+        L.rt_scene_opts_default.argtypes = [C.POINTER(SceneOpts)]
+        L.rt_scene_opts_default.restype = None
+        L.rt_scene_create.argtypes = [C.POINTER(MeshDesc), C.POINTER(SceneOpts), C.POINTER(vp)]
+        L.rt_scene_destroy.argtypes = [vp]
+        L.rt_scene_destroy.restype = None
+        L.rt_scene_get_info.argtypes = [vp, C.POINTER(SceneInfo)]
+        L.rt_scene_ref_boxes.argtypes = [vp, vp, vp, vp]
+        L.rt_camera_flycam.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, C.POINTER(Camera)]
+        L.rt_camera_flycam.restype = None
+        L.rt_render.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.POINTER(Frame), vp, C.POINTER(Stats)]
+        L.rt_render_async.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.POINTER(Frame)]
+        L.rt_synchronize.argtypes = [vp, C.POINTER(Stats)]
+        L.rt_frame_download.argtypes = [vp, vp, vp, vp]
+        L.rt_trace_closest.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp]
+        L.rt_trace_shadow.argtypes = [vp, C.c_int32, vp, vp, vp]
+        L.rt_debug_math_host.argtypes = [C.c_int32, C.c_int32, vp, vp]
+        L.rt_debug_math_device.argtypes = [C.c_int32, C.c_int32, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class RTError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        raise RTError(f"librtamd error {rc}: {lib().rt_last_error().decode()}")
+
+
+def device_count():
+    return lib().rt_device_count()
+
+
+class Mesh:
+    """Host-side Tucano-semantics mesh (rt_mesh)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @classmethod
+    def load_obj(cls, path):
+        h = C.c_void_p()
+        check(lib().rt_mesh_load_obj(os.fsencode(path), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_arrays(cls, v3, faces, materials, vn3=None, groups=None):
+        """materials: [nm, 12] (ka3 kd3 ks3 Ns Ni d). groups: [(n_faces, mat_id)]; default one group."""
+        v3 = np.ascontiguousarray(v3, np.float32)
+        faces = np.ascontiguousarray(faces, np.uint32).reshape(-1)
+        mats12 = np.ascontiguousarray(materials, np.float32).reshape(-1, 12)
+        if groups is None:
+            groups = [(len(faces) // 3, 0 if len(mats12) else -1)]
+        gc = np.array([3 * g[0] for g in groups], np.int32)
+        gm = np.array([g[1] for g in groups], np.int32)
+        mats = (Material * max(len(mats12), 1))()
+        for i, m in enumerate(mats12):
+            mats[i].ka[:] = list(m[0:3]); mats[i].kd[:] = list(m[3:6]); mats[i].ks[:] = list(m[6:9])
+            mats[i].shininess = float(m[9]); mats[i].optical_density = float(m[10]); mats[i].dissolve = float(m[11])
+        vn = None if vn3 is None else np.ascontiguousarray(vn3, np.float32)
+        h = C.c_void_p()
+        check(lib().rt_mesh_from_arrays(len(v3), _p(v3), _p(vn), len(gc), _p(gc), _p(faces), _p(gm), len(mats12),
+                                        C.cast(mats, C.c_void_p), C.byref(h)))
+        return cls(h)
+
+    def desc(self):
+        d = MeshDesc()
+        check(lib().rt_mesh_get_desc(self.h, C.byref(d)))
+        return d
+
+    def export(self):
+        d = self.desc()
+        nv, nf, nm = d.n_vertices, d.n_faces, d.n_materials
+
+        def arr(ptr, ctype, shape, dtype):
+            n = int(np.prod(shape))
+            if n == 0 or not ptr:
+                return np.zeros(shape, dtype)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(n,)).reshape(shape).astype(dtype).copy()
+
+        mats = []
+        if nm:
+            mp = C.cast(d.materials, C.POINTER(Material))
+            for i in range(nm):
+                m = mp[i]
+                mats.append(list(m.ka) + list(m.kd) + list(m.ks) + [m.shininess, m.optical_density, m.dissolve])
+        return dict(v4=arr(d.vertices, C.c_float, (nv, 4), np.float32),
+                    vn3=arr(d.vertex_normals, C.c_float, (nv, 3), np.float32),
+                    fidx=arr(d.face_vertex_ids, C.c_uint32, (nf, 3), np.uint32),
+                    fn3=arr(d.face_normals, C.c_float, (nf, 3), np.float32),
+                    fmat=arr(d.face_material_ids, C.c_int32, (nf,), np.int32),
+                    mats=np.array(mats, np.float32).reshape(-1, 12),
+                    M16=np.array(list(d.shape_model_matrix), np.float32))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.rt_mesh_destroy(self.h)
+            self.h = None
+
+
+def scene_opts(device=-1, min_faces=300, leaf_size=0):
+    o = SceneOpts()
+    lib().rt_scene_opts_default(C.byref(o))
+    o.device = device
+    o.min_faces = min_faces
+    o.leaf_size = leaf_size
+    return o
+
+
+class Scene:
+    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0):
+        self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
+        self.h = C.c_void_p()
+        d = mesh.desc()
+        o = scene_opts(device, min_faces, leaf_size)
+        check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
+
+    def info(self):
+        i = SceneInfo()
+        check(lib().rt_scene_get_info(self.h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in i._fields_}
+
+    def ref_boxes(self):
+        inf = self.info()
+        nb, nf = inf["n_ref_boxes"], inf["n_faces"]
+        b6 = np.zeros((nb, 6), np.float32)
+        cnt = np.zeros(nb, np.int32)
+        order = np.zeros(nf, np.int32)
+        check(lib().rt_scene_ref_boxes(self.h, _p(b6), _p(cnt), _p(order)))
+        return b6, cnt, order
+
+    @staticmethod
+    def _lights(lights):
+        arr = (Light * max(len(lights), 1))()
+        for i, (p, c) in enumerate(lights):
+            arr[i].position[:] = list(p)
+            arr[i].color[:] = list(c)
+        return arr
+
+    def render(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0, want_hits=False):
+        fr = Frame(W, H, mode, shard[0], shard[1], flags | (RT_FRAME_WRITE_HITS if want_hits else 0))
+        rgb = np.zeros((H, W, 3), np.float32)
+        st = Stats()
+        L = self._lights(lights)
+        check(lib().rt_render(self.h, C.byref(cam), C.cast(L, C.c_void_p), len(lights), C.byref(fr), _p(rgb),
+                              C.byref(st)))
+        if want_hits:
+            face = np.zeros((H, W), np.int32)
+            t = np.zeros((H, W), np.float32)
+            check(lib().rt_frame_download(self.h, None, _p(face), _p(t)))
+            return rgb, face, t, st.as_dict()
+        return rgb, st.as_dict()
+
+    def render_async(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0):
+        self._keep = self._lights(lights)
+        fr = Frame(W, H, mode, shard[0], shard[1], flags)
+        check(lib().rt_render_async(self.h, C.byref(cam), C.cast(self._keep, C.c_void_p), len(lights), C.byref(fr)))
+
+    def synchronize(self):
+        st = Stats()
+        check(lib().rt_synchronize(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def trace_closest(self, o, d):
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        n = len(o)
+        face = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        P = np.zeros((n, 3), np.float32)
+        check(lib().rt_trace_closest(self.h, n, _p(o), _p(d), _p(face), _p(t), _p(P)))
+        return face, t, P
+
+    def trace_shadow(self, P, L):
+        P = np.ascontiguousarray(P, np.float32).reshape(-1, 3)
+        L = np.ascontiguousarray(L, np.float32).reshape(-1, 3)
+        out = np.zeros(len(P), np.int32)
+        check(lib().rt_trace_shadow(self.h, len(P), _p(P), _p(L), _p(out)))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.rt_scene_destroy(self.h)
+            self.h = None
+
+
+def flycam(W, H, dx=0.0, dy=0.0, dz=0.0):
+    c = Camera()
+    lib().rt_camera_flycam(W, H, dx, dy, dz, C.byref(c))
+    return c
+
+
+def generate_soup(n_tris, seed=12345):
+    v = np.zeros((3 * n_tris, 3), np.float32)
+    lib().rt_generate_soup(n_tris, seed, _p(v))
+    return v
+
+
+def write_ppm(path, rgb):
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    H, W = rgb.shape[:2]
+    check(lib().rt_write_ppm(os.fsencode(path), _p(rgb), W, H))
+
+
+def debug_math(op, inp, n, out_len, device=False):
+    out = np.zeros(n * out_len, np.float32)
+    inp = np.ascontiguousarray(inp, np.float32)
+    f = lib().rt_debug_math_device if device else lib().rt_debug_math_host
+    check(f(op, n, _p(inp), _p(out)))
+    return out
+
+
+DEFAULT_LIGHTS = [((-0.5, 2.0, 3.0), (1.0, 1.0, 1.0))]  # flyscene.cpp:37
+SOUP_MATERIAL = [0.1, 0.1, 0.1, 0.7, 0.7, 0.7, 0.2, 0.2, 0.2, 16.0, 1.0, 1.0]  # C3/C4
+
+
+def soup_mesh(n_tris, seed=12345):
+    v = generate_soup(n_tris, seed)
+    f = np.arange(3 * n_tris, dtype=np.uint32).reshape(-1, 3)
+    return Mesh.from_arrays(v, f, np.array([SOUP_MATERIAL], np.float32)), v, f

@@ -1,0 +1,129 @@
+"""CPU tests of the product library's host side (no GPU needed): the C-ABI loads and exports every
+declared symbol, and the host-side stages of the path (Tucano ingest, camera, reference box
+partition, BVH build, PPM writer, Eigen-order math) agree bit for bit with the pinned oracle."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, scene_path
+from test_oracle_pinning import read_kat, same_bits
+
+HEADER = os.path.join(ROOT, "include", "rt", "rt_api.h")
+SCENES = ["cube", "plane", "testding", "cornell", "dodgeColorTest", "bunny"]
+
+
+def test_header_symbols_exported(rt):
+    decl = set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", open(HEADER).read()))
+    assert decl == set(rt.EXPORTS), decl ^ set(rt.EXPORTS)
+    L = rt.lib()
+    for name in sorted(decl):
+        assert hasattr(L, name), name
+    assert L.rt_version() == 1
+
+
+def test_no_device_is_reported_not_faked(rt):
+    # in the CPU container there is no GPU: render entry points must fail loudly
+    if rt.device_count() > 0:
+        pytest.skip("GPU visible")
+    mesh = rt.Mesh.load_obj(scene_path("cube.obj"))
+    with pytest.raises(rt.RTError, match="no HIP device"):
+        rt.Scene(mesh)
+    sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
+    with pytest.raises(rt.RTError, match="host-only"):
+        sc.render(rt.flycam(64, 64), rt.DEFAULT_LIGHTS, 64, 64)
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_ingest_matches_oracle(rt, orc, name):
+    a = rt.Mesh.load_obj(scene_path(name + ".obj")).export()
+    b = orc.Mesh.load_obj(scene_path(name + ".obj")).export()
+    for k in ("v4", "vn3", "fidx", "fn3", "fmat", "mats", "M16"):
+        assert a[k].shape == b[k].shape, k
+        assert same_bits(a[k], b[k]).all() if a[k].dtype == np.float32 else (a[k] == b[k]).all(), k
+
+
+def test_soup_generator_matches_oracle(rt, orc):
+    a = rt.generate_soup(20000, 12345)
+    b = orc.generate_soup(20000, 12345)
+    assert a.tobytes() == b.tobytes()
+    assert np.abs(a).max() <= 0.51
+
+
+@pytest.mark.parametrize("dxyz", [(0, 0, 0), (0, 0, 20), (3, -2, 7)])
+@pytest.mark.parametrize("WH", [(256, 256), (1920, 1080), (37, 11)])
+def test_camera_matches_oracle(rt, orc, dxyz, WH):
+    a = rt.flycam(*WH, *dxyz)
+    b = orc.flycam(*WH, *dxyz)
+    for f in ("view", "viewport"):
+        pass
+    assert list(a.view_matrix) == list(b.view)
+    assert list(a.viewport) == list(b.viewport)
+    assert a.fovy == b.fovy and a.aspect_ratio == b.aspect
+
+
+@pytest.mark.parametrize("sec", read_kat(), ids=lambda s: f"op{s[0]}")
+def test_host_math_matches_eigen(rt, sec):
+    op, n, il, ol, inp, exp = sec
+    got = rt.debug_math(op, inp, n, ol, device=False)
+    bad = (~same_bits(got, exp)).reshape(n, ol).any(1)
+    assert bad.sum() == 0, f"op {op}: {bad.sum()} cases differ"
+
+
+@pytest.mark.parametrize("name", ["cube", "dodgeColorTest", "bunny"])
+def test_reference_boxes_match_oracle(rt, orc, name):
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path(name + ".obj")), device=rt.RT_DEVICE_NONE)
+    osc = orc.Scene(orc.Mesh.load_obj(scene_path(name + ".obj")))
+    b6, cnt, order = sc.ref_boxes()
+    ob6, ocnt, oorder = osc.boxes()
+    assert len(cnt) == len(ocnt)
+    assert (cnt == ocnt).all() and (order == oorder).all()
+    assert same_bits(b6, ob6).all()
+
+
+def test_reference_boxes_soup_match_oracle(rt, orc):
+    n = 200000
+    mesh, v, f = rt.soup_mesh(n)
+    sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
+    om = orc.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32))
+    osc = orc.Scene(om)
+    b6, cnt, order = sc.ref_boxes()
+    ob6, ocnt, oorder = osc.boxes()
+    assert (cnt == ocnt).all() and (order == oorder).all() and same_bits(b6, ob6).all()
+    info = sc.info()
+    assert info["n_ref_boxes"] == len(ocnt)
+    assert 0 < info["bvh_depth"] <= 60
+    assert info["bvh_nodes"] >= 1 and info["bvh_leaves"] >= n // 16
+
+
+def test_bvh_bounds_sane_for_empty_and_single(rt):
+    # a single triangle and a one-leaf scene build a valid root
+    v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
+    mesh = rt.Mesh.from_arrays(v, np.array([[0, 1, 2]], np.uint32), np.array([rt.SOUP_MATERIAL], np.float32))
+    info = rt.Scene(mesh, device=rt.RT_DEVICE_NONE).info()
+    assert info["n_faces"] == 1 and info["bvh_nodes"] == 1 and info["n_ref_boxes"] == 1
+    empty = rt.Mesh.from_arrays(np.zeros((0, 3), np.float32), np.zeros((0, 3), np.uint32),
+                                np.array([rt.SOUP_MATERIAL], np.float32), groups=[])
+    info = rt.Scene(empty, device=rt.RT_DEVICE_NONE).info()
+    assert info["n_faces"] == 0 and info["bvh_nodes"] == 0
+
+
+def test_ppm_writer_format(rt, tmp_path):
+    rgb = np.array([[[0.0, 0.5, 1.0], [1.5, -0.25, 0.999]]], np.float32)
+    p = tmp_path / "x.ppm"
+    rt.write_ppm(str(p), rgb)
+    # writePPMImage: "P3\nW H\n255\n", min(255,(int)(255*c)) with " " after each value, "\n" per row
+    assert p.read_text() == "P3\n2 1\n255\n0 127 255 255 -63 254 \n"
+
+
+def test_invalid_inputs_rejected(rt, tmp_path):
+    with pytest.raises(rt.RTError, match="Cannot open"):
+        rt.Mesh.load_obj(str(tmp_path / "missing.obj"))
+    bad = tmp_path / "bad.obj"
+    bad.write_text("v 0 0 0\nv 1 0 0\nf 1 2\n")
+    with pytest.raises(rt.RTError, match="multiple of 3"):
+        rt.Mesh.load_obj(str(bad))
+    bad.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 9\n")
+    with pytest.raises(rt.RTError, match="out of range"):
+        rt.Mesh.load_obj(str(bad))
