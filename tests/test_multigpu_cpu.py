@@ -1,0 +1,88 @@
+"""Multi-GPU path on CPU: the tile partition used across ranks, the gloo-backed timing reductions
+bench.py performs (world_size 2), and that per-rank renders stitch to the single-device frame
+(oracle as the renderer, since the CPU container has no GPU)."""
+import importlib.util
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT, scene_path
+
+spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+bench = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(bench)
+
+
+@pytest.mark.parametrize("WH", [(1920, 1080), (3840, 2160), (37, 11), (8, 8)])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_tile_partition_is_exact_cover(WH, n):
+    W, H = WH
+    seen = {}
+    for r in range(n):
+        for t in bench.shard_tiles(W, H, r, n):
+            assert t not in seen
+            seen[t] = r
+    assert len(seen) == ((W + 7) // 8) * ((H + 7) // 8)
+    counts = np.bincount(list(seen.values()), minlength=n)
+    assert counts.max() - counts.min() <= 1  # interleaving balances tile counts
+
+
+def test_weak_scaling_frames():
+    for n, (W, H) in {1: (1920, 1080), 4: (3840, 2160)}.items():
+        assert bench.frame_for(n, None)[:2] == (W, H)
+    for n in (2, 8):
+        W, H, kind = bench.frame_for(n, None)
+        assert kind == "weak" and abs(W * H / n / (1920 * 1080) - 1) < 0.01
+    assert bench.frame_for(8, "3840x2160") == (3840, 2160, "strong")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    reduce = bench.make_reducer(dist, torch.device("cpu"))
+    dist.barrier()
+    q.put((rank, reduce(1.0 + rank, "MAX"), reduce(100.0 * (rank + 1), "SUM")))
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_timing_reduction():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [2.0, 2.0]       # max over ranks of elapsed
+    assert [r[2] for r in res] == [300.0, 300.0]   # whole-job rays
+
+
+def test_sharded_renders_stitch_to_full_frame(orc):
+    W, H, n = 44, 30, 3
+    sc = orc.Scene(orc.Mesh.load_obj(scene_path("cube.obj")))
+    cam = orc.flycam(W, H)
+    full, _, _ = sc.render(cam, orc.DEFAULT_LIGHTS, W, H)
+    out = np.full((H, W, 3), np.nan, np.float32)
+    for r in range(n):
+        pix = [(x, y) for tx, ty in bench.shard_tiles(W, H, r, n)
+               for y in range(ty * 8, min(H, ty * 8 + 8)) for x in range(tx * 8, min(W, tx * 8 + 8))]
+        rgb, _, _ = sc.render(cam, orc.DEFAULT_LIGHTS, W, H, pixels=pix)
+        for (x, y), c in zip(pix, rgb):
+            out[y, x] = c
+    assert out.tobytes() == full.reshape(H, W, 3).tobytes()

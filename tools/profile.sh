@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 evidence for the bench kernel (run on the GPU box): kernel-trace + stats, then separate
+# --pmc passes (never combined with tracing domains). Output under gpurun_out/prof/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+ARGS="${BENCH_ARGS:---steps 20 --warmup 5 --no-cpu}"
+timeout -k 10 120 rocprofv3 -L > $OUT/counters_avail.txt 2>&1 || true
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
+    python3 bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace.err
+rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
+i=0
+for set in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD" "TCC_HIT_sum TCC_MISS_sum" \
+           ${EXTRA_PMC:-}; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set -d $OUT/pmc$i -o run --output-format csv -- \
+      python3 bench.py --steps 5 --warmup 1 --no-cpu --no-stats > $OUT/pmc$i.json 2> $OUT/pmc$i.err
+  rc=$?; echo "pmc$i ($set) rc=$rc"
+  case $rc in 124|134|137|139) exit $rc;; esac
+done
+exit 0

@@ -1,0 +1,73 @@
+"""Summarise a tools/profile.sh run (gpurun_out/prof) into profiles/<tag>_*.
+
+Writes:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_pmc.json           per-counter mean over the render-kernel dispatches + derived figures
+HBM traffic follows /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide streaming reads, so it is doubled;
+both are collected in separate passes.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_render<0, false, false, false>"):
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    stats_src = os.path.join(prof, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats_src, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    avg_ns = None
+    for r in csv.DictReader(open(stats_src)):
+        if kernel in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+    counters = defaultdict(list)
+    for d in sorted(os.listdir(prof)):
+        f = os.path.join(prof, d, "run_counter_collection.csv")
+        if d.startswith("pmc") and os.path.exists(f):
+            for r in csv.DictReader(open(f)):
+                if kernel in r["Kernel_Name"]:
+                    counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    mean = {k: sum(v) / len(v) for k, v in counters.items()}
+    out = {"kernel": kernel, "avg_kernel_ns_trace": avg_ns, "counters_mean_per_dispatch": mean,
+           "dispatches_per_counter": {k: len(v) for k, v in counters.items()}}
+    bench = os.path.join(prof, "trace_bench.json")
+    if os.path.exists(bench):
+        try:
+            out["bench_line_under_trace"] = json.loads(open(bench).read().strip().splitlines()[-1])
+        except Exception:
+            pass
+    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+        fetch = 2.0 * mean["FETCH_SIZE"] * 1024
+        write = mean["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = fetch + write
+        out["hbm_read_bytes_per_launch_corrected"] = fetch
+        out["hbm_write_bytes_per_launch"] = write
+        if avg_ns:
+            out["hbm_GBps"] = (fetch + write) / avg_ns
+    if "GRBM_GUI_ACTIVE" in mean and avg_ns:
+        out["effective_clock_GHz"] = mean["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+    if "SQ_WAVE_CYCLES" in mean:
+        wc = mean["SQ_WAVE_CYCLES"]
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in mean:
+                out[f"frac_{k}"] = mean[k] / wc
+    if "TCC_HIT_sum" in mean and "TCC_MISS_sum" in mean:
+        out["l2_hit_rate"] = mean["TCC_HIT_sum"] / (mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"])
+    if "SQ_WAVES" in mean:
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD"):
+            if k in mean:
+                out[f"{k}_per_wave"] = mean[k] / mean["SQ_WAVES"]
+    out["tag"] = tag
+    path = os.path.join(ROOT, "profiles", f"{tag}_pmc.json")
+    json.dump(out, open(path, "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_latest.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "bench_line_under_trace"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
