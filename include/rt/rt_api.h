@@ -147,7 +147,8 @@ typedef struct rt_frame {
   int32_t width, height;
   int32_t mode;        /* RT_MODE_PRIMARY: closest hit + unshadowed Phong (traceRay at depth limit 1);
                           RT_MODE_FULL: reference traceRay as-is (shadow per light + 1 reflection) */
-  int32_t shard_index; /* this device renders the 8x8 tiles t with t % shard_count == shard_index */
+  int32_t shard_index; /* this device renders the 16x16 tiles t (row-major over the frame) with
+                          t % shard_count == shard_index */
   int32_t shard_count; /* 1 = whole frame */
   int32_t flags;       /* RT_FRAME_* */
 } rt_frame;
@@ -159,6 +160,8 @@ typedef struct rt_stats {
   double kernel_ms;         /* device time of the render kernels since the previous rt_synchronize,
                                summed over launches (HIP events on the scene's stream) */
   int64_t launches;         /* render launches covered by kernel_ms */
+  double trace_kernel_ms;   /* part of kernel_ms spent in the traversal kernel (PRIMARY: first of the
+                               two kernels of a frame; FULL: the whole single kernel) */
   int64_t primary_rays;     /* pixels traced by this call */
   int64_t total_rays;       /* primary + shadow + reflection rays issued */
   int64_t hits;             /* primary rays that hit */

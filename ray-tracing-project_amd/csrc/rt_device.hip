@@ -60,9 +60,10 @@ __device__ __forceinline__ T sload64(const T* base, uint32_t i) {
 }
 __device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t i) { return sload64(base, i); }
 __device__ __forceinline__ TriRec64 sload_tri(const TriRec64* base, uint32_t i) { return sload64(base, i); }
+
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
 // counters of the RT_FRAME_STATS counting run
@@ -122,16 +123,32 @@ __device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]};
 // Rare path of a candidate (uniform triangle): interpolated normal non-zero (calculateDistance's
 // norm()==0 check, flyscene.cpp:467) and the reference box predicate. All loads wave-uniform.
 __device__ __forceinline__ bool accept_candidate(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0, f3 a1,
-                                                f3 a2, const Ray& r) {
-  const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
-  const float area = norm(cross(e0, neg(e2))) / 2;
-  const uint32_t* fs = P.fshade + 4 * (size_t)tr.face;
-  const f3 n0 = ld3(P.vnorm + 4 * (size_t)fs[0]);
-  const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs[1]);
-  const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs[2]);
-  const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
-  if (norm(nn) == 0) return false;
-  return ref_box_test(r, P.refbox + 8 * (size_t)tr.box);
+                                                f3 a2, f3 p, const Ray& r, bool cand) {
+  if (!(tr.box & kSafeNormalBit)) {  // uniform branch: only faces the host could not certify
+    const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
+    const float area = norm(cross(e0, neg(e2))) / 2;
+    const uint32_t* fs = P.fshade + 4 * (size_t)tr.face;
+    const f3 n0 = ld3(P.vnorm + 4 * (size_t)fs[0]);
+    const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs[1]);
+    const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs[2]);
+    const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
+    cand = cand & (norm(nn) != 0);
+  }
+  // reference box predicate. Fast path: the object-space hit point lies inside the reference box
+  // with a margin (1e-5 relative) far above the reference slab test's rounding, so the exact ray
+  // crosses the box interior at t >= 0 and intersectBox accepts. Otherwise run the exact test.
+  const float* bx = P.refbox + 8 * (size_t)(tr.box & ~kSafeNormalBit);
+  const f3 X = affv3(P.Minv, p);
+  const float lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[4], bx[5], bx[6]};
+  const float xs[3] = {X.x, X.y, X.z}, os[3] = {r.o2.x, r.o2.y, r.o2.z};
+  bool inside = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float m = 1e-5f * ((hi[k] - lo[k]) + fabsf(lo[k]) + fabsf(hi[k]) + fabsf(os[k])) + 1e-30f;
+    inside = inside & (xs[k] > lo[k] + m) & (xs[k] < hi[k] - m);
+  }
+  if (!ballot(cand & !inside)) return cand;
+  return cand & (inside | ref_box_test(r, bx));
 }
 
 // calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record.
@@ -144,26 +161,24 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
   const float dn = dot(n, r.d);                 // facenormal.dot(dir)
   const float orth = tr.dist - dot(r.o, n);     // distancePlane - origin.dot(facenormal)
   const float t = orth / dn;                    // / dir.dot(facenormal)  (same bits as dn)
+  // predicates combined with bitwise ops: no per-lane branches (exec-mask traffic is SALU work)
   bool cand;
-  if (ANY) cand = active && dn != 0.0f && t >= 0.0f;
-  else cand = active && dn != 0.0f && t >= 0.0f && t < INFINITY && (t < h.t || (t == h.t && tr.rank < h.rank));
+  if (ANY) cand = active & (dn != 0.0f) & (t >= 0.0f);
+  else cand = active & (dn != 0.0f) & (t >= 0.0f) & (t < INFINITY) & ((t < h.t) | ((t == h.t) & (tr.rank < h.rank)));
   if (!ballot(cand)) return;
   const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  cand = cand && !(dot(n, a0) < 0 || dot(n, a1) < 0 || dot(n, a2) < 0);
+  cand = cand & !((dot(n, a0) < 0) | (dot(n, a1) < 0) | (dot(n, a2) < 0));
   if (!ballot(cand)) return;
-  if (cand) {
-    if (accept_candidate(P, tr, e0, e2, a0, a1, a2, r)) {
-      if (ANY) {
-        found = true;
-      } else {
-        h.t = t;
-        h.rank = tr.rank;
-        h.slot = slot;
-      }
-    }
+  const bool acc = accept_candidate(P, tr, e0, e2, a0, a1, a2, p, r, cand);
+  if (ANY) {
+    found = found | acc;
+  } else {
+    h.t = acc ? t : h.t;
+    h.rank = acc ? tr.rank : h.rank;
+    h.slot = acc ? slot : h.slot;
   }
 }
 
@@ -177,17 +192,21 @@ struct WaveStack {
 };
 
 template <bool ANY, bool STATS, bool STACK_LDS>
-__device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found, uint32_t* lds_stack,
-                         uint32_t* cnt) {
+__device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                         uint32_t* lds_stack, uint32_t* cnt) {
   if (P.n_nodes == 0) return;
-  WaveStack st;
+  uint32_t stackv = 0;     // lane k holds stack entry k (VGPR stack)
+  int sp = 0;              // wave-uniform stack depth (SGPR)
   uint64_t flagstack = 0;  // STATS: per-lane "my ray wanted this entry" bit per stack level
   bool want = active;      // STATS: this lane's ray intersects the current node
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
   for (;;) {
     if (!is_leaf(node)) {
-      const Node64 nd = sload_node(P.nodes, node);
+      const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
+      // keep the child handles in the same fetch/wait as the boxes (hipcc otherwise sinks a second
+      // dependent s_load for them below the ballot branch)
+      asm volatile("" ::"s"(nd.child0), "s"(nd.child1));
       if (STATS) {
         if (want) cnt[ST_NODE]++;
         cnt[ST_WNODE]++;
@@ -196,35 +215,35 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       bool h0, h1;
       const float t0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut, h0);
       const float t1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut, h1);
-      h0 = h0 && active;
-      h1 = h1 && active;
+      h0 = h0 & active;
+      h1 = h1 & active;
       const uint64_t m0 = ballot(h0), m1 = ballot(h1);
-      if (m0 && m1) {
-        const uint64_t v0 = ballot(h0 && (!h1 || t0 <= t1));
-        const uint64_t v1 = ballot(h1 && (!h0 || t1 < t0));
-        const bool first0 = __popcll(v0) >= __popcll(v1);
+      if ((m0 | m1) == 0) {  // no lane needs either child
+        if (sp == 0) break;
+        sp--;
+        node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
+        if (STATS) want = (flagstack >> sp) & 1;
+        continue;
+      }
+      // near child first by lane majority: each lane that needs a child votes for the one it enters first
+      const uint64_t v0 = ballot(h0 & (!h1 | (t0 <= t1)));
+      const bool first0 = (m1 == 0) | ((m0 != 0) & (2 * __popcll(v0) >= __popcll(m0 | m1)));
+      const uint32_t near = first0 ? nd.child0 : nd.child1;
+      if ((m0 != 0) & (m1 != 0)) {
         const uint32_t far = first0 ? nd.child1 : nd.child0;
-        node = first0 ? nd.child0 : nd.child1;
-        if (STACK_LDS) lds_stack[st.sp] = far;
-        else st.v = (lane_id() == st.sp) ? far : st.v;  // v_cmp + v_cndmask: lane sp holds the entry
+        if (STACK_LDS) lds_stack[sp] = far;
+        else stackv = (lane_id() == sp) ? far : stackv;  // v_cmp + v_cndmask
         if (STATS) {
           const bool wf = first0 ? h1 : h0;
-          flagstack = (flagstack & ~(1ull << st.sp)) | ((uint64_t)wf << st.sp);
-          want = first0 ? h0 : h1;
+          flagstack = (flagstack & ~(1ull << sp)) | ((uint64_t)wf << sp);
         }
-        st.sp++;
-      } else if (m0 | m1) {
-        node = m0 ? nd.child0 : nd.child1;
-        if (STATS) want = m0 ? h0 : h1;
-      } else {
-        if (st.sp == 0) break;
-        st.sp--;
-        node = STACK_LDS ? uniform(lds_stack[st.sp]) : (uint32_t)__builtin_amdgcn_readlane(st.v, st.sp);
-        if (STATS) want = (flagstack >> st.sp) & 1;
+        sp++;
       }
+      if (STATS) want = first0 ? h0 : h1;
+      node = near;
       continue;
     }
-    // leaf: test its triangles against every lane
+    // leaf: its triangles are fetched once per wave and tested by every lane
     const uint32_t first = leaf_first(node), count = leaf_count(node);
     if (STATS) {
       if (want) cnt[ST_TRI] += count;
@@ -235,13 +254,13 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       test_tri<ANY>(P, tr, first + k, r, active, h, found);
     }
     if (ANY) {
-      active = active && !found;
+      active = active & !found;
       if (!ballot(active)) break;
     }
-    if (st.sp == 0) break;
-    st.sp--;
-    node = STACK_LDS ? uniform(lds_stack[st.sp]) : (uint32_t)__builtin_amdgcn_readlane(st.v, st.sp);
-    if (STATS) want = (flagstack >> st.sp) & 1;
+    if (sp == 0) break;
+    sp--;
+    node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
+    if (STATS) want = (flagstack >> sp) & 1;
   }
 }
 
@@ -335,37 +354,125 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
 }
 
 // ------------------------------------------------------------------------------------------------
-// Render kernel: one wave per 8x8 tile of this shard
+// Frame kernels. One block = one 16x16 pixel tile (2x2 waves of 8x8, one ray per lane).
+// XCD-aware order: blocks b and b+8 share an XCD under round-robin dispatch, so each XCD gets a
+// contiguous run of tiles (L2 reuse; speed only, any placement is correct).
 // ------------------------------------------------------------------------------------------------
-template <int MODE, bool STATS, bool HITS, bool STACK_LDS>
-__global__ __launch_bounds__(256) void k_render(FrameParams P) {
-  __shared__ uint32_t lds_stacks[STACK_LDS ? 4 : 1][64];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int wave = (int)uniform(blockIdx.x * 4 + wv);
-  if (wave >= P.n_tiles_shard) return;
-  uint32_t* lds_stack = lds_stacks[STACK_LDS ? wv : 0];
-  const int tile = P.shard_index + wave * P.shard_count;
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
-  const bool active = px < P.W && py < P.H;
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+struct PixelCoord {
+  int px, py, wv, lane;
+  bool active;
+};
 
-  // traceRayThread: o = getCenter(), d = normalize(screenToWorld(i, j) - o)   (flyscene.cpp:301-308)
-  Ray r;
-  {
-    const float nx = (float)(2.0 * (double)((float)px - P.vp[0]) / (double)P.vp[2] - 1.0);
-    const float ny = (float)(1.0 - 2.0 * (double)((float)py - P.vp[1]) / (double)P.vp[3]);
-    const f3 w = affv3(P.vinv, f3{nx * P.xscale, ny * P.yscale, -1.0f});
-    r.o = f3{P.eye[0], P.eye[1], P.eye[2]};
-    r.d = normalized(sub(w, r.o));
-    r.o2 = f3{P.eye_obj[0], P.eye_obj[1], P.eye_obj[2]};
-    r.d2 = normalized(m3v3(P.MS, r.d));
-    setup_cull(r);
+__device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
+  PixelCoord c;
+  c.lane = threadIdx.x & 63;
+  c.wv = (int)uniform(threadIdx.x >> 6);
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  int L = b;
+  if (P.xcd_remap) {
+    const int q = nb >> 3, rr = nb & 7, x = b & 7, k = b >> 3;
+    L = x < rr ? x * (q + 1) + k : rr * (q + 1) + (x - rr) * q + k;
   }
+  const int tile = P.shard_index + L * P.shard_count;
+  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  c.px = tx * 16 + (c.wv & 1) * 8 + (c.lane & 7);
+  c.py = ty * 16 + (c.wv >> 1) * 8 + (c.lane >> 3);
+  c.active = c.px < P.W && c.py < P.H;
+  return c;
+}
+
+// traceRayThread: o = getCenter(), d = normalize(screenToWorld(i, j) - o)   (flyscene.cpp:301-308;
+// Camera::screenToWorld camera.hpp:155-173 with its fp64 NDC)
+__device__ __forceinline__ Ray primary_ray(const FrameParams& P, int px, int py) {
+  Ray r;
+  const float nx = (float)(2.0 * (double)((float)px - P.vp[0]) / (double)P.vp[2] - 1.0);
+  const float ny = (float)(1.0 - 2.0 * (double)((float)py - P.vp[1]) / (double)P.vp[3]);
+  const f3 w = affv3(P.vinv, f3{nx * P.xscale, ny * P.yscale, -1.0f});
+  r.o = f3{P.eye[0], P.eye[1], P.eye[2]};
+  r.d = normalized(sub(w, r.o));
+  r.o2 = f3{P.eye_obj[0], P.eye_obj[1], P.eye_obj[2]};
+  r.d2 = normalized(m3v3(P.MS, r.d));
+  setup_cull(r);
+  return r;
+}
+
+__device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t* cnt, int lane) {
+#pragma unroll
+  for (int c = 0; c < ST_COUNT; c++) {
+    unsigned long long v = cnt[c];
+    if (c == ST_WNODE || c == ST_WTRI) v = (lane == 0) ? v : 0;  // wave fetches counted once
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0 && v) atomicAdd(P.stats + c, v);
+  }
+}
+
+// PRIMARY stage 1: closest hit per pixel (calculateMinimumFace, flyscene.cpp:373-396) -> 8-B hit record.
+// Only traversal state is live here, so the kernel fits 8 waves per SIMD.
+template <bool STATS, bool STACK_LDS>
+__global__ __launch_bounds__(256) void k_trace_primary(FrameParams P) {
+  __shared__ uint32_t lds_stacks[STACK_LDS ? 4 : 1][64];
+  const PixelCoord c = pixel_coord(P);
+  uint32_t* lds_stack = lds_stacks[STACK_LDS ? c.wv : 0];
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  const Ray r = primary_ray(P, c.px, c.py);
+  if (STATS && c.active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
+  Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  bool dummy = false;
+  traverse<false, STATS, STACK_LDS>(P.sc, r, c.active, h, dummy, lds_stack, cnt);
+  if (STATS && c.active && h.t != INFINITY) cnt[ST_HITS]++;
+  if (c.active) P.hits[(size_t)c.py * P.W + c.px] = make_uint2(__float_as_uint(h.t), h.slot);
+  if (STATS) flush_stats(P, cnt, c.lane);
+}
+
+// PRIMARY stage 2: traceRay at depth limit 1 without shadows: calculateColor (flyscene.cpp:603-614)
+// + traceRay's ks update and clamp (:355-370), or the background on a miss (:327-332).
+template <bool HITS>
+__global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
+  const PixelCoord c = pixel_coord(P);
+  if (!c.active) return;
+  const size_t pix = (size_t)c.py * P.W + c.px;
+  const uint2 hb = P.hits[pix];
+  const float t = __uint_as_float(hb.x);
+  const bool hit0 = t != INFINITY;
+  f3 col;
+  int32_t face = -1;
+  if (hit0) {
+    const Ray r = primary_ray(P, c.px, c.py);
+    const TriRec64 tr0 = vload_tri(P.sc.tris, hb.y);
+    HitInfo hi0;
+    hi0.face = tr0.face;
+    face = (int32_t)tr0.face;
+    hi0.p = f3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
+    hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
+    MatState st = load_mat(P.defmat);
+    const f3 direct0 = calc_color<false, false, false>(P, st, hi0, r.o, true, nullptr, nullptr);
+    if (hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;
+    col = f3{clamp01(direct0.x + 0.0f * st.ks.x), clamp01(direct0.y + 0.0f * st.ks.y),
+             clamp01(direct0.z + 0.0f * st.ks.z)};
+  } else {
+    col = f3{P.bg[0], P.bg[1], P.bg[2]};
+  }
+  P.rgb[3 * pix + 0] = col.x;
+  P.rgb[3 * pix + 1] = col.y;
+  P.rgb[3 * pix + 2] = col.z;
+  if (HITS) {
+    P.face_out[pix] = face;
+    P.t_out[pix] = t;
+  }
+}
+
+// FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
+// bounce, all in one kernel (flyscene.cpp:317-371, 510-566, 603-614).
+template <bool STATS, bool HITS, bool STACK_LDS>
+__global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
+  __shared__ uint32_t lds_stacks[STACK_LDS ? 4 : 1][64];
+  const PixelCoord c = pixel_coord(P);
+  const bool active = c.active;
+  uint32_t* lds_stack = lds_stacks[STACK_LDS ? c.wv : 0];
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
 
-  // calculateMinimumFace (flyscene.cpp:373-396)
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
   traverse<false, STATS, STACK_LDS>(P.sc, r, active, h, dummy, lds_stack, cnt);
@@ -374,51 +481,47 @@ __global__ __launch_bounds__(256) void k_render(FrameParams P) {
 
   MatState st = load_mat(P.defmat);
   HitInfo hi0;
-  TriRec64 tr0;
   hi0.mat = -1;
   hi0.face = 0xFFFFFFFFu;
   hi0.p = f3{0.0f, 0.0f, 0.0f};
   hi0.n = f3{0.0f, 0.0f, 0.0f};
   if (hit0) {
-    tr0 = vload_tri(P.sc.tris, h.slot);
+    const TriRec64 tr0 = vload_tri(P.sc.tris, h.slot);
     hi0.face = tr0.face;
     hi0.p = f3{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
     hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
   }
-  constexpr bool FULL = MODE == RT_MODE_FULL;
-  const f3 direct0 = calc_color<FULL, STATS, STACK_LDS>(P, st, hi0, r.o, hit0, lds_stack, cnt);
+  const f3 direct0 = calc_color<true, STATS, STACK_LDS>(P, st, hi0, r.o, hit0, lds_stack, cnt);
   if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
 
-  f3 refl{0.0f, 0.0f, 0.0f};  // traceRay(depth+1): 0 at the depth limit (PRIMARY) or on a miss
-  if (FULL) {
-    // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
-    Ray rr;
-    rr.d = reflect(normalized(r.d), hi0.n);
-    rr.o = offset(hi0.p, rr.d, 0.001f);
-    rr.o2 = affv3(P.Minv, rr.o);
-    rr.d2 = normalized(m3v3(P.MS, rr.d));
-    setup_cull(rr);
-    if (STATS && hit0) cnt[ST_TOTAL]++;
-    Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    traverse<false, STATS, STACK_LDS>(P.sc, rr, hit0, h1, dummy, lds_stack, cnt);
-    const bool hit1 = hit0 && h1.t != INFINITY;
-    HitInfo hi1;
-    hi1.mat = -1;
-    hi1.p = f3{0.0f, 0.0f, 0.0f};
-    hi1.n = f3{0.0f, 0.0f, 0.0f};
-    if (hit1) {
-      const TriRec64 tr1 = vload_tri(P.sc.tris, h1.slot);
-      hi1.face = tr1.face;
-      hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
-      hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
-    }
-    const f3 direct1 = calc_color<true, STATS, STACK_LDS>(P, st, hi1, rr.o, hit1, lds_stack, cnt);
-    if (hit1) {
-      if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
-      // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
-      refl = f3{clamp01(direct1.x + 0.0f * st.ks.x), clamp01(direct1.y + 0.0f * st.ks.y),
-                clamp01(direct1.z + 0.0f * st.ks.z)};
-    }
+  // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
+  f3 refl{0.0f, 0.0f, 0.0f};
+  Ray rr;
+  rr.d = reflect(normalized(r.d), hi0.n);
+  rr.o = offset(hi0.p, rr.d, 0.001f);
+  rr.o2 = affv3(P.Minv, rr.o);
+  rr.d2 = normalized(m3v3(P.MS, rr.d));
+  setup_cull(rr);
+  if (STATS && hit0) cnt[ST_TOTAL]++;
+  Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  traverse<false, STATS, STACK_LDS>(P.sc, rr, hit0, h1, dummy, lds_stack, cnt);
+  const bool hit1 = hit0 && h1.t != INFINITY;
+  HitInfo hi1;
+  hi1.mat = -1;
+  hi1.p = f3{0.0f, 0.0f, 0.0f};
+  hi1.n = f3{0.0f, 0.0f, 0.0f};
+  if (hit1) {
+    const TriRec64 tr1 = vload_tri(P.sc.tris, h1.slot);
+    hi1.face = tr1.face;
+    hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
+    hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
+  }
+  const f3 direct1 = calc_color<true, STATS, STACK_LDS>(P, st, hi1, rr.o, hit1, lds_stack, cnt);
+  if (hit1) {
+    if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
+    // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
+    refl = f3{clamp01(direct1.x + 0.0f * st.ks.x), clamp01(direct1.y + 0.0f * st.ks.y),
+              clamp01(direct1.z + 0.0f * st.ks.z)};
   }
   f3 col;
   if (hit0) {
@@ -428,24 +531,16 @@ __global__ __launch_bounds__(256) void k_render(FrameParams P) {
     col = f3{P.bg[0], P.bg[1], P.bg[2]};
   }
   if (active) {
-    const size_t pix = (size_t)py * P.W + px;
+    const size_t pix = (size_t)c.py * P.W + c.px;
     P.rgb[3 * pix + 0] = col.x;
     P.rgb[3 * pix + 1] = col.y;
     P.rgb[3 * pix + 2] = col.z;
     if (HITS) {
       P.face_out[pix] = hit0 ? (int32_t)hi0.face : -1;
-      P.t_out[pix] = active ? h.t : INFINITY;
+      P.t_out[pix] = h.t;
     }
   }
-  if (STATS) {
-#pragma unroll
-    for (int c = 0; c < ST_COUNT; c++) {
-      unsigned long long v = cnt[c];
-      if (c == ST_WNODE || c == ST_WTRI) v = (lane == 0) ? v : 0;  // wave fetches counted once
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0 && v) atomicAdd(P.stats + c, v);
-    }
-  }
+  if (STATS) flush_stats(P, cnt, c.lane);
 }
 
 // Ray-list kernels (rt_trace_closest / rt_trace_shadow), 64 rays per wave
@@ -473,7 +568,7 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
   setup_cull(r);
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool found = false;
-  traverse<ANY, false, false>(P.sc, r, active, h, found, lds_stacks[threadIdx.x >> 6], nullptr);
+  traverse<ANY, false, true>(P.sc, r, active, h, found, lds_stacks[threadIdx.x >> 6], nullptr);
   if (!active) return;
   if (ANY) {
     R.blocked[i] = found ? 1 : 0;
@@ -566,7 +661,7 @@ void device_release(rt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
   void* bufs[] = {s->d_nodes, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats,
-                  s->d_rgb, s->d_face, s->d_t};
+                  s->d_rgb, s->d_face, s->d_t, s->d_hits};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
@@ -586,6 +681,7 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.mats = s->d_mats;
   P.sc.root = hs.root;
   P.sc.n_nodes = (int32_t)hs.nodes.size();
+  memcpy(P.sc.Minv, hs.Minv, 64);
   memcpy(P.Minv, hs.Minv, 64);
   memcpy(P.MS, hs.MS, 36);
   const rt_material& dm = s->opts.default_material;
@@ -599,17 +695,36 @@ static int ensure_fb(rt_scene* s, size_t npix) {
   if (s->d_rgb) (void)hipFree(s->d_rgb);
   if (s->d_face) (void)hipFree(s->d_face);
   if (s->d_t) (void)hipFree(s->d_t);
-  s->d_rgb = nullptr; s->d_face = nullptr; s->d_t = nullptr;
+  if (s->d_hits) (void)hipFree(s->d_hits);
+  s->d_rgb = nullptr; s->d_face = nullptr; s->d_t = nullptr; s->d_hits = nullptr;
   HIPCHECK(hipMalloc((void**)&s->d_rgb, npix * 12));
   HIPCHECK(hipMalloc((void**)&s->d_face, npix * 4));
   HIPCHECK(hipMalloc((void**)&s->d_t, npix * 4));
+  HIPCHECK(hipMalloc((void**)&s->d_hits, npix * 8));
   s->fb_pixels = npix;
   return RT_OK;
 }
 
-template <int MODE, bool STATS, bool HITS>
-static void launch_render(const FrameParams& P, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((k_render<MODE, STATS, HITS, false>), dim3(grid), dim3(256), 0, st, P);
+// variant bits (debug knob RT_KERNEL_VARIANT, for A/B measurements; 0 = the measured-best default):
+// 1 = lane-register (VGPR) stack instead of the LDS stack, 4 = XCD-aware tile order
+template <bool STATS>
+static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int variant) {
+  if (variant & 1) hipLaunchKernelGGL((k_trace_primary<STATS, false>), dim3(grid), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL((k_trace_primary<STATS, true>), dim3(grid), dim3(256), 0, st, P);
+}
+template <bool STATS, bool HITS>
+static void launch_full(const FrameParams& P, int grid, hipStream_t st, int variant) {
+  if (variant & 1) hipLaunchKernelGGL((k_render_full<STATS, HITS, false>), dim3(grid), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL((k_render_full<STATS, HITS, true>), dim3(grid), dim3(256), 0, st, P);
+}
+
+static int kernel_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RT_KERNEL_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
 }
 
 }  // namespace rt
@@ -669,8 +784,8 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   }
   P.W = fr->width;
   P.H = fr->height;
-  P.tiles_x = (fr->width + 7) / 8;
-  P.tiles_y = (fr->height + 7) / 8;
+  P.tiles_x = (fr->width + 15) / 16;
+  P.tiles_y = (fr->height + 15) / 16;
   const int ntiles = P.tiles_x * P.tiles_y;
   P.shard_index = si;
   P.shard_count = sc;
@@ -681,31 +796,42 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   P.face_out = s->d_face;
   P.t_out = s->d_t;
   P.stats = s->d_stats;
+  P.hits = s->d_hits;
   hipStream_t st = (hipStream_t)s->stream;
   const bool stats = (fr->flags & RT_FRAME_STATS) != 0;
   const bool hits = (fr->flags & RT_FRAME_WRITE_HITS) != 0;
   if (stats) HIPCHECK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st));
-  const int grid = (P.n_tiles_shard + 3) / 4;
-  if (s->ev_used + 2 > s->ev_pool.size()) {
-    if (s->ev_pool.size() >= 4096) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }
-    for (int k = 0; k < 2; k++) {
+  const int grid = P.n_tiles_shard;
+  const int variant = kernel_variant();
+  P.xcd_remap = (variant & 4) ? 1 : 0;
+  if (s->ev_used + 3 > s->ev_pool.size()) {
+    if (s->ev_pool.size() >= 3 * 2048) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }
+    for (int k = 0; k < 3; k++) {
       hipEvent_t e;
       HIPCHECK(hipEventCreate(&e));
       s->ev_pool.push_back(e);
     }
   }
-  hipEvent_t ev_a = (hipEvent_t)s->ev_pool[s->ev_used], ev_b = (hipEvent_t)s->ev_pool[s->ev_used + 1];
-  s->ev_used += 2;
+  // three events per frame: start | after the traversal kernel | after the frame
+  hipEvent_t ev_a = (hipEvent_t)s->ev_pool[s->ev_used], ev_m = (hipEvent_t)s->ev_pool[s->ev_used + 1],
+             ev_b = (hipEvent_t)s->ev_pool[s->ev_used + 2];
+  s->ev_used += 3;
   HIPCHECK(hipEventRecord(ev_a, st));
   if (grid > 0) {
     if (fr->mode == RT_MODE_PRIMARY) {
-      if (stats) { if (hits) launch_render<RT_MODE_PRIMARY, true, true>(P, grid, st); else launch_render<RT_MODE_PRIMARY, true, false>(P, grid, st); }
-      else { if (hits) launch_render<RT_MODE_PRIMARY, false, true>(P, grid, st); else launch_render<RT_MODE_PRIMARY, false, false>(P, grid, st); }
+      if (stats) launch_trace<true>(P, grid, st, variant); else launch_trace<false>(P, grid, st, variant);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipEventRecord(ev_m, st));
+      if (hits) hipLaunchKernelGGL(k_shade_primary<true>, dim3(grid), dim3(256), 0, st, P);
+      else hipLaunchKernelGGL(k_shade_primary<false>, dim3(grid), dim3(256), 0, st, P);
     } else {
-      if (stats) { if (hits) launch_render<RT_MODE_FULL, true, true>(P, grid, st); else launch_render<RT_MODE_FULL, true, false>(P, grid, st); }
-      else { if (hits) launch_render<RT_MODE_FULL, false, true>(P, grid, st); else launch_render<RT_MODE_FULL, false, false>(P, grid, st); }
+      if (stats) { if (hits) launch_full<true, true>(P, grid, st, variant); else launch_full<true, false>(P, grid, st, variant); }
+      else { if (hits) launch_full<false, true>(P, grid, st, variant); else launch_full<false, false>(P, grid, st, variant); }
+      HIPCHECK(hipEventRecord(ev_m, st));
     }
     HIPCHECK(hipGetLastError());
+  } else {
+    HIPCHECK(hipEventRecord(ev_m, st));
   }
   HIPCHECK(hipEventRecord(ev_b, st));
   s->last_W = fr->width;
@@ -715,7 +841,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   int64_t rays = 0;
   for (int t = si; t < ntiles; t += sc) {
     const int tx = t % P.tiles_x, ty = t / P.tiles_x;
-    rays += (int64_t)std::min(8, fr->width - tx * 8) * std::min(8, fr->height - ty * 8);
+    rays += (int64_t)std::min(16, fr->width - tx * 16) * std::min(16, fr->height - ty * 16);
   }
   s->last_rays = rays;
   s->pending = true;
@@ -729,14 +855,17 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
   struct Reset { rt_scene* s; ~Reset() { s->ev_used = 0; s->pending = false; } } reset_{s};
   if (out) {
     memset(out, 0, sizeof *out);
-    double tot = 0.0;
-    for (size_t k = 0; k + 1 < s->ev_used; k += 2) {
-      float ms = 0.0f;
-      HIPCHECK(hipEventElapsedTime(&ms, (hipEvent_t)s->ev_pool[k], (hipEvent_t)s->ev_pool[k + 1]));
+    double tot = 0.0, trav = 0.0;
+    for (size_t k = 0; k + 3 <= s->ev_used; k += 3) {
+      float ms = 0.0f, ms1 = 0.0f;
+      HIPCHECK(hipEventElapsedTime(&ms, (hipEvent_t)s->ev_pool[k], (hipEvent_t)s->ev_pool[k + 2]));
+      HIPCHECK(hipEventElapsedTime(&ms1, (hipEvent_t)s->ev_pool[k], (hipEvent_t)s->ev_pool[k + 1]));
       tot += ms;
+      trav += ms1;
     }
     out->kernel_ms = tot;
-    out->launches = (int64_t)(s->ev_used / 2);
+    out->trace_kernel_ms = trav;
+    out->launches = (int64_t)(s->ev_used / 3);
     out->primary_rays = s->last_rays;
     out->total_rays = s->last_rays;
     if (s->last_flags & RT_FRAME_STATS) {
@@ -776,12 +905,12 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* ligh
   if (sc == 1) return rt_frame_download(s, out_rgb, nullptr, nullptr);
   std::vector<float> full((size_t)W * H * 3);
   if ((rc = rt_frame_download(s, full.data(), nullptr, nullptr))) return rc;
-  const int tiles_x = (W + 7) / 8, ntiles = tiles_x * ((H + 7) / 8);
+  const int tiles_x = (W + 15) / 16, ntiles = tiles_x * ((H + 15) / 16);
   for (int t = fr->shard_index; t < ntiles; t += sc) {
     const int tx = t % tiles_x, ty = t / tiles_x;
-    for (int y = ty * 8; y < std::min(H, ty * 8 + 8); y++) {
-      const size_t o = ((size_t)y * W + tx * 8) * 3;
-      memcpy(out_rgb + o, full.data() + o, sizeof(float) * 3 * (size_t)(std::min(W, tx * 8 + 8) - tx * 8));
+    for (int y = ty * 16; y < std::min(H, ty * 16 + 16); y++) {
+      const size_t o = ((size_t)y * W + tx * 16) * 3;
+      memcpy(out_rgb + o, full.data() + o, sizeof(float) * 3 * (size_t)(std::min(W, tx * 16 + 16) - tx * 16));
     }
   }
   return RT_OK;

@@ -650,6 +650,29 @@ struct BvhBuilder {
 };
 }  // namespace
 
+// A face whose interpolated normal (interpolateNormal, flyscene.cpp:594-599) can never be the zero
+// vector for a point that passed the inside test: its area A (same expression the kernel uses) is a
+// positive normal number and every unit vertex normal leans into the face normal (n.nk >= 0.5). Then
+// n.(sum_k nk a_k / A) >= 0.5 (sum a_k)/A >= 0.5 (sub-areas of a point in the plane sum to >= A),
+// far above rounding, so norm() != 0 and the reference never rejects the face for it; when A would
+// overflow the blend, the result is NaN, which the reference also accepts (NaN != 0).
+static bool safe_normal(const HostScene& hs, uint32_t f) {
+  const f3& w0 = hs.wv[hs.fidx[3 * f]];
+  const f3& w1 = hs.wv[hs.fidx[3 * f + 1]];
+  const f3& w2 = hs.wv[hs.fidx[3 * f + 2]];
+  const f3 e0 = sub(w1, w0), e2 = sub(w0, w2);
+  const float A = norm(cross(e0, neg(e2))) / 2;
+  if (!(A > 1e-30f) || !std::isfinite(A)) return false;
+  const f3& n = hs.fnn[f];
+  for (int k = 0; k < 3; k++) {
+    const f3& nk = hs.vnn[hs.fidx[3 * f + k]];
+    if (!std::isfinite(nk.x) || !std::isfinite(nk.y) || !std::isfinite(nk.z)) return false;
+    if (std::fabs(sqnorm(nk) - 1.0f) > 1e-3f) return false;
+    if (!(dot(n, nk) >= 0.5f)) return false;
+  }
+  return true;
+}
+
 void build_bvh(HostScene& hs, int leaf_size) {
   hs.nodes.clear();
   hs.tris.clear();
@@ -734,7 +757,7 @@ void build_bvh(HostScene& hs, int leaf_size) {
     r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
     r.rank = hs.face_rank[f];
     r.face = f;
-    r.box = hs.face_box[f];
+    r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u);
   }
 }
 

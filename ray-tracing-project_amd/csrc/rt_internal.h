@@ -12,6 +12,11 @@
 // Frame buffers: rgb float[H][W][3]; optional face int32[H][W], t float[H][W]; stats counters.
 #pragma once
 #include <cstdint>
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#else
+struct uint2 { unsigned int x, y; };
+#endif
 
 #include "rt_math.h"
 
@@ -22,6 +27,9 @@ constexpr uint32_t kLeafCountShift = 27;          // 4 bits: count - 1 (1..16 tr
 constexpr uint32_t kLeafFirstMask = (1u << 27) - 1;  // first triangle slot (< 134M)
 constexpr int kMaxLeaf = 16;
 constexpr int kMaxDepth = 60;  // wave stack holds 64 entries; occupancy <= depth
+// TriRec64::box bit 31: the triangle's interpolated normal can never be the zero vector (see
+// rt_host.cpp safe_normal()), so calculateDistance's norm()==0 rejection never fires for it
+constexpr uint32_t kSafeNormalBit = 0x80000000u;
 
 RT_HD bool is_leaf(uint32_t h) { return (h & kLeafBit) != 0; }
 RT_HD uint32_t leaf_first(uint32_t h) { return h & kLeafFirstMask; }
@@ -46,7 +54,7 @@ struct alignas(16) TriRec64 {
   float w2z;
   uint32_t rank;  // position in the reference's (box, in-box) iteration order: tie-break key
   uint32_t face;  // original mesh face index
-  uint32_t box;   // reference box holding the face (intersectBox predicate)
+  uint32_t box;   // reference box holding the face (intersectBox predicate) | kSafeNormalBit
 };
 static_assert(sizeof(TriRec64) == 64, "triangle record must be 64 bytes");
 
@@ -70,6 +78,7 @@ struct DevScene {
   const DevMat* mats;
   uint32_t root;           // root handle; n_nodes == 0 -> empty scene
   int32_t n_nodes;
+  float Minv[16];          // getShapeModelMatrix().inverse() (object-space hit point for the box fast path)
 };
 
 // Per-launch parameters (kernel argument, ~1 KB)
@@ -89,13 +98,15 @@ struct FrameParams {
   int32_t n_lights;
   Light lights[16];
   // frame
-  int32_t W, H, tiles_x, tiles_y;
+  int32_t W, H, tiles_x, tiles_y;  // tiles = 16x16 pixel blocks (one 256-thread block each)
+  int32_t xcd_remap;
   int32_t shard_index, shard_count, n_tiles_shard;
   int32_t mode, flags;
   float* rgb;
   int32_t* face_out;
   float* t_out;
   unsigned long long* stats;  // [8] counters (RT_FRAME_STATS)
+  uint2* hits;                // [H][W] (t bits, triangle slot): PRIMARY trace -> shade hand-off
 };
 
 // Ray-list query parameters (rt_trace_closest / rt_trace_shadow)

@@ -72,6 +72,7 @@ struct rt_scene {
   float* d_rgb = nullptr;
   int32_t* d_face = nullptr;
   float* d_t = nullptr;
+  uint2* d_hits = nullptr;
   size_t fb_pixels = 0;
   int32_t last_W = 0, last_H = 0, last_flags = 0;
   int64_t last_rays = 0, last_total_rays = 0;

@@ -65,7 +65,8 @@ class Frame(C.Structure):
 
 
 class Stats(C.Structure):
-    _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_int64), ("primary_rays", C.c_int64), ("total_rays", C.c_int64),
+    _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_int64), ("trace_kernel_ms", C.c_double),
+                ("primary_rays", C.c_int64), ("total_rays", C.c_int64),
                 ("hits", C.c_int64), ("node_visits", C.c_int64), ("tri_tests", C.c_int64),
                 ("wave_node_fetches", C.c_int64), ("wave_tri_fetches", C.c_int64)]
 

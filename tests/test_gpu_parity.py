@@ -116,10 +116,10 @@ def test_soup_shards_stitch_bitwise(rt, soup):
         for k in range(n):
             part, st = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, shard=(k, n))
             tiles = np.zeros((H, W), bool)
-            tx = (W + 7) // 8
-            for tt in range(k, tx * ((H + 7) // 8), n):
-                x, y = (tt % tx) * 8, (tt // tx) * 8
-                tiles[y:y + 8, x:x + 8] = True
+            tx = (W + 15) // 16
+            for tt in range(k, tx * ((H + 15) // 16), n):
+                x, y = (tt % tx) * 16, (tt // tx) * 16
+                tiles[y:y + 16, x:x + 16] = True
             out[tiles] = part[tiles]
         assert out.tobytes() == ref.tobytes(), n
 

@@ -27,7 +27,7 @@ def test_tile_partition_is_exact_cover(WH, n):
         for t in bench.shard_tiles(W, H, r, n):
             assert t not in seen
             seen[t] = r
-    assert len(seen) == ((W + 7) // 8) * ((H + 7) // 8)
+    assert len(seen) == ((W + 15) // 16) * ((H + 15) // 16)
     counts = np.bincount(list(seen.values()), minlength=n)
     assert counts.max() - counts.min() <= 1  # interleaving balances tile counts
 
@@ -81,7 +81,7 @@ def test_sharded_renders_stitch_to_full_frame(orc):
     out = np.full((H, W, 3), np.nan, np.float32)
     for r in range(n):
         pix = [(x, y) for tx, ty in bench.shard_tiles(W, H, r, n)
-               for y in range(ty * 8, min(H, ty * 8 + 8)) for x in range(tx * 8, min(W, tx * 8 + 8))]
+               for y in range(ty * 16, min(H, ty * 16 + 16)) for x in range(tx * 16, min(W, tx * 16 + 16))]
         rgb, _, _ = sc.render(cam, orc.DEFAULT_LIGHTS, W, H, pixels=pix)
         for (x, y), c in zip(pix, rgb):
             out[y, x] = c
