@@ -89,17 +89,24 @@ __device__ __forceinline__ void setup_cull(Ray& r) {
   r.oid = f3{-r.o.x * r.id.x, -r.o.y * r.id.y, -r.o.z * r.id.z};
 }
 
-// Conservative slab test for one padded child box (culling only; exactness comes from padding)
-__device__ __forceinline__ float slab(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
-                                      float tmax_ray, bool& hit) {
+// Conservative slab test for one padded child box (culling only; exactness comes from padding):
+// returns the entry distance tmin and the exit distance clipped to [0, tmax_ray] (hit iff tmin <= tmax)
+struct Span {
+  float tmin, tmax;
+};
+__device__ __forceinline__ Span slab(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
+                                     float tmax_ray) {
   const float tx0 = __builtin_fmaf(lx, r.id.x, r.oid.x), tx1 = __builtin_fmaf(hx, r.id.x, r.oid.x);
   const float ty0 = __builtin_fmaf(ly, r.id.y, r.oid.y), ty1 = __builtin_fmaf(hy, r.id.y, r.oid.y);
   const float tz0 = __builtin_fmaf(lz, r.id.z, r.oid.z), tz1 = __builtin_fmaf(hz, r.id.z, r.oid.z);
-  const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-  const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_ray));
-  hit = tmin <= tmax;
-  return tmin;
+  Span s;
+  s.tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  s.tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_ray));
+  return s;
 }
+// lane masks straight from v_cmp (no bool materialisation): llvm.amdgcn.fcmp predicates
+constexpr int kFcmpOLE = 5;
+__device__ __forceinline__ uint64_t mask_le(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOLE); }
 
 // The reference's object-space box test, exact (flyscene.cpp:484-507)
 __device__ __forceinline__ bool ref_box_test(const Ray& r, const float* bx) {
@@ -201,6 +208,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
   bool want = active;      // STATS: this lane's ray intersects the current node
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
+  uint64_t act = ballot(active);  // lanes still tracing (wave-uniform mask)
   for (;;) {
     if (!is_leaf(node)) {
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
@@ -212,12 +220,9 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
         cnt[ST_WNODE]++;
       }
       const float tcut = ANY ? tmax_any : h.t;
-      bool h0, h1;
-      const float t0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut, h0);
-      const float t1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut, h1);
-      h0 = h0 & active;
-      h1 = h1 & active;
-      const uint64_t m0 = ballot(h0), m1 = ballot(h1);
+      const Span s0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
+      const Span s1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+      const uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
       if ((m0 | m1) == 0) {  // no lane needs either child
         if (sp == 0) break;
         sp--;
@@ -226,9 +231,10 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
         continue;
       }
       // near child first by lane majority: each lane that needs a child votes for the one it enters first
-      const uint64_t v0 = ballot(h0 & (!h1 | (t0 <= t1)));
+      const uint64_t v0 = m0 & (~m1 | mask_le(s0.tmin, s1.tmin));
       const bool first0 = (m1 == 0) | ((m0 != 0) & (2 * __popcll(v0) >= __popcll(m0 | m1)));
       const uint32_t near = first0 ? nd.child0 : nd.child1;
+      const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
       if ((m0 != 0) & (m1 != 0)) {
         const uint32_t far = first0 ? nd.child1 : nd.child0;
         if (STACK_LDS) lds_stack[sp] = far;
@@ -255,7 +261,8 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
     }
     if (ANY) {
       active = active & !found;
-      if (!ballot(active)) break;
+      act = ballot(active);
+      if (!act) break;
     }
     if (sp == 0) break;
     sp--;
