@@ -43,19 +43,19 @@ namespace rt {
 // uniform (scalar) loads: a generic pointer re-typed into the constant address space makes hipcc
 // emit s_load_dwordx16 for wave-uniform indices (one fetch per wave, data in SGPRs)
 // ------------------------------------------------------------------------------------------------
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(4))) f4v* cf4p;
+typedef int i16v __attribute__((ext_vector_type(16)));
 
+// One s_load_dwordx16 per 64-B record (hipcc otherwise splits the record into x4/x8 pieces, one
+// scalar-cache request each, and sinks parts below the first use). The wait is inside the asm
+// because the compiler does not track the counter of an inline-asm load.
 template <typename T>
 __device__ __forceinline__ T sload64(const T* base, uint32_t i) {
   static_assert(sizeof(T) == 64, "64-byte records");
-  const cf4p p = (cf4p)(base) + 4 * (size_t)i;
-  const f4v a = p[0], b = p[1], c = p[2], d = p[3];
+  const T* p = base + __builtin_amdgcn_readfirstlane(i);
+  i16v v;
+  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   T r;
-  __builtin_memcpy(reinterpret_cast<char*>(&r) + 0, &a, 16);
-  __builtin_memcpy(reinterpret_cast<char*>(&r) + 16, &b, 16);
-  __builtin_memcpy(reinterpret_cast<char*>(&r) + 32, &c, 16);
-  __builtin_memcpy(reinterpret_cast<char*>(&r) + 48, &d, 16);
+  __builtin_memcpy(&r, &v, 64);
   return r;
 }
 __device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t i) { return sload64(base, i); }
@@ -212,9 +212,6 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
   for (;;) {
     if (!is_leaf(node)) {
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
-      // keep the child handles in the same fetch/wait as the boxes (hipcc otherwise sinks a second
-      // dependent s_load for them below the ballot branch)
-      asm volatile("" ::"s"(nd.child0), "s"(nd.child1));
       if (STATS) {
         if (want) cnt[ST_NODE]++;
         cnt[ST_WNODE]++;
@@ -269,6 +266,147 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
     node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
     if (STATS) want = (flagstack >> sp) & 1;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// 4-wide traversal over the quantised nodes (Node4Q). Per node one scalar 64-B fetch; every lane
+// slab-tests the four children against the dequantised boxes (origin + q * 2^e, rounded outward on
+// the host, so culling stays conservative). The nearest hit child (entry distance seen by the first
+// interested lane) is visited next; the other hit children go onto the LDS wave stack, farthest
+// deepest.
+// ------------------------------------------------------------------------------------------------
+// SALU select of child i (0..3) without control flow
+__device__ __forceinline__ uint32_t pick4(uint32_t i, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  uint32_t a, b;
+  asm("s_bitcmp1_b32 %2, 0\n\t"
+      "s_cselect_b32 %0, %4, %3\n\t"
+      "s_cselect_b32 %1, %6, %5\n\t"
+      "s_bitcmp1_b32 %2, 1\n\t"
+      "s_cselect_b32 %0, %1, %0"
+      : "=&s"(a), "=&s"(b)
+      : "s"(i), "s"(c0), "s"(c1), "s"(c2), "s"(c3)
+      : "scc");
+  return a;
+}
+__device__ __forceinline__ uint32_t rdlane(float v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(v), lane);
+}
+// all-ones / zero 64-bit lane mask from bit c of a uniform byte
+__device__ __forceinline__ uint64_t bitmask64(uint32_t bits, int c) {
+  const uint32_t m = (uint32_t)((int32_t)(bits << (31 - c)) >> 31);
+  return ((uint64_t)m << 32) | m;
+}
+
+template <bool ANY, bool STATS>
+__device__ __forceinline__ void traverse4(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                          uint32_t* lds_stack, uint64_t* lds_mask, uint32_t* cnt) {
+  if (P.n_nodes == 0) return;
+  int sp = 0;
+  bool want = active;
+  uint32_t node = P.root4;
+  uint64_t act = ballot(active);
+  // lanes 0..3 stand for children 0..3 when the far children are pushed (lanes >= 3 duplicate 3)
+  const int lc = lane_id() < 3 ? lane_id() : 3;
+  for (;;) {
+    if (!is_leaf(node)) {
+      const Node4Q nd = sload64(P.nodes4, node);
+      if (STATS) {
+        if (want) cnt[ST_NODE]++;
+        cnt[ST_WNODE]++;
+      }
+      const float tcut = ANY ? INFINITY : h.t;
+      const float sx = __uint_as_float((uint32_t)nd.ex << 23) * r.id.x;
+      const float sy = __uint_as_float((uint32_t)nd.ey << 23) * r.id.y;
+      const float sz = __uint_as_float((uint32_t)nd.ez << 23) * r.id.z;
+      const float bx = __builtin_fmaf(nd.ox, r.id.x, r.oid.x);
+      const float by = __builtin_fmaf(nd.oy, r.id.y, r.oid.y);
+      const float bz = __builtin_fmaf(nd.oz, r.id.z, r.oid.z);
+      uint64_t m[4];
+      float tm[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float tx0 = __builtin_fmaf((float)((nd.qlx >> (8 * c)) & 255u), sx, bx);
+        const float tx1 = __builtin_fmaf((float)((nd.qhx >> (8 * c)) & 255u), sx, bx);
+        const float ty0 = __builtin_fmaf((float)((nd.qly >> (8 * c)) & 255u), sy, by);
+        const float ty1 = __builtin_fmaf((float)((nd.qhy >> (8 * c)) & 255u), sy, by);
+        const float tz0 = __builtin_fmaf((float)((nd.qlz >> (8 * c)) & 255u), sz, bz);
+        const float tz1 = __builtin_fmaf((float)((nd.qhz >> (8 * c)) & 255u), sz, bz);
+        const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+        const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcut));
+        m[c] = mask_le(tmin, tmax) & act & bitmask64(nd.valid, c);
+        tm[c] = tmin;
+      }
+      const uint64_t any = m[0] | m[1] | m[2] | m[3];
+      if (any == 0) {
+        if (sp == 0) break;
+        sp--;
+        node = uniform(lds_stack[sp]);
+        if (STATS) want = (lds_mask[sp] >> lane_id()) & 1;
+        continue;
+      }
+      // keys: entry distance seen by the first interested lane (tmin >= 0, so its bits order as
+      // uint32), child index in the low two bits; children nobody needs sort last
+      const int rep = (int)__builtin_ctzll(any);
+      uint32_t k[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) k[c] = m[c] ? ((rdlane(tm[c], rep) & ~3u) | (uint32_t)c) : 0xFFFFFFFFu;
+      const uint32_t kmin = uniform(min(min(k[0], k[1]), min(k[2], k[3])));
+      const int nhit = (int)__builtin_popcount(((m[0] != 0) ? 1u : 0u) | ((m[1] != 0) ? 2u : 0u) |
+                                               ((m[2] != 0) ? 4u : 0u) | ((m[3] != 0) ? 8u : 0u));
+      if (nhit > 1) {
+        // lane c (c < 4) writes child c at sp + ((nhit - 1 - rank_c) & 3): the far children land
+        // farthest-deepest below the new top, the near child and the unused ones above it
+        const uint32_t myk = lc == 0 ? k[0] : (lc == 1 ? k[1] : (lc == 2 ? k[2] : k[3]));
+        const int rank = (k[0] < myk) + (k[1] < myk) + (k[2] < myk) + (k[3] < myk);
+        const int pos = sp + ((nhit - 1 - rank) & 3);
+        lds_stack[pos] = lc == 0 ? nd.child[0] : (lc == 1 ? nd.child[1] : (lc == 2 ? nd.child[2] : nd.child[3]));
+        if (STATS) lds_mask[pos] = lc == 0 ? m[0] : (lc == 1 ? m[1] : (lc == 2 ? m[2] : m[3]));
+        sp += nhit - 1;
+      }
+      node = pick4(kmin & 3, nd.child[0], nd.child[1], nd.child[2], nd.child[3]);
+      if (STATS) {
+        const uint32_t ci = kmin & 3;
+        want = (((ci == 0) ? m[0] : (ci == 1) ? m[1] : (ci == 2) ? m[2] : m[3]) >> lane_id()) & 1;
+      }
+      continue;
+    }
+    const uint32_t first = leaf_first(node), count = leaf_count(node);
+    if (STATS) {
+      if (want) cnt[ST_TRI] += count;
+      cnt[ST_WTRI] += count;
+    }
+    for (uint32_t q = 0; q < count; q++) {
+      const TriRec64 tr = sload_tri(P.tris, first + q);
+      test_tri<ANY>(P, tr, first + q, r, active, h, found);
+    }
+    if (ANY) {
+      active = active & !found;
+      act = ballot(active);
+      if (!act) break;
+    }
+    if (sp == 0) break;
+    sp--;
+    node = uniform(lds_stack[sp]);
+    if (STATS) want = (lds_mask[sp] >> lane_id()) & 1;
+  }
+}
+
+// Traversal flavours (A/B knob RT_KERNEL_VARIANT): binary nodes with the VGPR or the LDS stack, or
+// the 4-wide quantised nodes
+enum { TRAV_B2_VGPR = 0, TRAV_B2_LDS = 1, TRAV_W4 = 2 };
+
+template <int TRAV, bool STATS>
+struct WaveLds {
+  static constexpr int kEntries = TRAV == TRAV_W4 ? kStack4 : 64;
+  uint32_t stack[4][kEntries];
+  uint64_t mask[4][(STATS && TRAV == TRAV_W4) ? kEntries : 1];
+};
+
+template <bool ANY, bool STATS, int TRAV>
+__device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                      WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
+  if (TRAV == TRAV_W4) traverse4<ANY, STATS>(P, r, active, h, found, L.stack[wv], L.mask[STATS ? wv : 0], cnt);
+  else traverse<ANY, STATS, TRAV == TRAV_B2_LDS>(P, r, active, h, found, L.stack[wv], cnt);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -334,9 +472,9 @@ __device__ __forceinline__ float clamp01(float x) { return smax(smin(x, 1.0f), 0
 
 // calculateColor (flyscene.cpp:603-614). SHADOWS: per light, a wave-packet any-hit traversal from
 // P + 0.003 L (box predicate from P) decides whether the light contributes (calcSingleColor :543).
-template <bool SHADOWS, bool STATS, bool STACK_LDS>
+template <bool SHADOWS, bool STATS, int TRAV>
 __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, const HitInfo& hi, f3 o, bool lane_hit,
-                         uint32_t* lds_stack, uint32_t* cnt) {
+                                         WaveLds<TRAV, STATS>* lds, int wv, uint32_t* cnt) {
   f3 sum{0.0f, 0.0f, 0.0f};
   for (int l = 0; l < P.n_lights; l++) {
     const float* lp = P.lights[l].p;
@@ -351,7 +489,7 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       setup_cull(sr);
       Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if (STATS && lane_hit) cnt[ST_TOTAL]++;
-      traverse<true, STATS, STACK_LDS>(P.sc, sr, lane_hit, hh, blocked, lds_stack, cnt);
+      trace<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
     }
     f3 c{0.0f, 0.0f, 0.0f};
     if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
@@ -415,17 +553,16 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
 
 // PRIMARY stage 1: closest hit per pixel (calculateMinimumFace, flyscene.cpp:373-396) -> 8-B hit record.
 // Only traversal state is live here, so the kernel fits 8 waves per SIMD.
-template <bool STATS, bool STACK_LDS>
+template <bool STATS, int TRAV>
 __global__ __launch_bounds__(256) void k_trace_primary(FrameParams P) {
-  __shared__ uint32_t lds_stacks[STACK_LDS ? 4 : 1][64];
+  __shared__ WaveLds<TRAV, STATS> lds;
   const PixelCoord c = pixel_coord(P);
-  uint32_t* lds_stack = lds_stacks[STACK_LDS ? c.wv : 0];
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && c.active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  traverse<false, STATS, STACK_LDS>(P.sc, r, c.active, h, dummy, lds_stack, cnt);
+  trace<false, STATS, TRAV>(P.sc, r, c.active, h, dummy, lds, c.wv, cnt);
   if (STATS && c.active && h.t != INFINITY) cnt[ST_HITS]++;
   if (c.active) P.hits[(size_t)c.py * P.W + c.px] = make_uint2(__float_as_uint(h.t), h.slot);
   if (STATS) flush_stats(P, cnt, c.lane);
@@ -452,7 +589,7 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
     hi0.p = f3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
     hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
     MatState st = load_mat(P.defmat);
-    const f3 direct0 = calc_color<false, false, false>(P, st, hi0, r.o, true, nullptr, nullptr);
+    const f3 direct0 = calc_color<false, false, TRAV_B2_LDS>(P, st, hi0, r.o, true, nullptr, 0, nullptr);
     if (hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;
     col = f3{clamp01(direct0.x + 0.0f * st.ks.x), clamp01(direct0.y + 0.0f * st.ks.y),
              clamp01(direct0.z + 0.0f * st.ks.z)};
@@ -470,19 +607,18 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
 
 // FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
 // bounce, all in one kernel (flyscene.cpp:317-371, 510-566, 603-614).
-template <bool STATS, bool HITS, bool STACK_LDS>
+template <bool STATS, bool HITS, int TRAV>
 __global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
-  __shared__ uint32_t lds_stacks[STACK_LDS ? 4 : 1][64];
+  __shared__ WaveLds<TRAV, STATS> lds;
   const PixelCoord c = pixel_coord(P);
   const bool active = c.active;
-  uint32_t* lds_stack = lds_stacks[STACK_LDS ? c.wv : 0];
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
 
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  traverse<false, STATS, STACK_LDS>(P.sc, r, active, h, dummy, lds_stack, cnt);
+  trace<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, c.wv, cnt);
   const bool hit0 = active && h.t != INFINITY;
   if (STATS && hit0) cnt[ST_HITS]++;
 
@@ -498,7 +634,7 @@ __global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
     hi0.p = f3{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
     hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
   }
-  const f3 direct0 = calc_color<true, STATS, STACK_LDS>(P, st, hi0, r.o, hit0, lds_stack, cnt);
+  const f3 direct0 = calc_color<true, STATS, TRAV>(P, st, hi0, r.o, hit0, &lds, c.wv, cnt);
   if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
 
   // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
@@ -511,7 +647,7 @@ __global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
   setup_cull(rr);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  traverse<false, STATS, STACK_LDS>(P.sc, rr, hit0, h1, dummy, lds_stack, cnt);
+  trace<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, c.wv, cnt);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
   hi1.mat = -1;
@@ -523,7 +659,7 @@ __global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
     hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
     hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
   }
-  const f3 direct1 = calc_color<true, STATS, STACK_LDS>(P, st, hi1, rr.o, hit1, lds_stack, cnt);
+  const f3 direct1 = calc_color<true, STATS, TRAV>(P, st, hi1, rr.o, hit1, &lds, c.wv, cnt);
   if (hit1) {
     if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
     // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
@@ -551,9 +687,9 @@ __global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
 }
 
 // Ray-list kernels (rt_trace_closest / rt_trace_shadow), 64 rays per wave
-template <bool ANY>
+template <bool ANY, int TRAV>
 __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
-  __shared__ uint32_t lds_stacks[4][64];
+  __shared__ WaveLds<TRAV, false> lds;
   const int lane = threadIdx.x & 63;
   const int base = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * 64);
   if (base >= R.n) return;
@@ -575,7 +711,7 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
   setup_cull(r);
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool found = false;
-  traverse<ANY, false, true>(P.sc, r, active, h, found, lds_stacks[threadIdx.x >> 6], nullptr);
+  trace<ANY, false, TRAV>(P.sc, r, active, h, found, lds, (int)uniform(threadIdx.x >> 6), nullptr);
   if (!active) return;
   if (ANY) {
     R.blocked[i] = found ? 1 : 0;
@@ -632,6 +768,7 @@ int device_upload(rt_scene* s) {
   tot = 0;
   int rc;
   if ((rc = dalloc_copy(&s->d_nodes, hs.nodes.data(), hs.nodes.size() * sizeof(Node64), tot))) return rc;
+  if ((rc = dalloc_copy(&s->d_nodes4, hs.nodes4.data(), hs.nodes4.size() * sizeof(Node4Q), tot))) return rc;
   if ((rc = dalloc_copy(&s->d_tris, hs.tris.data(), hs.tris.size() * sizeof(TriRec64), tot))) return rc;
   std::vector<uint32_t> fshade(4 * (size_t)hs.nf);
   for (int32_t f = 0; f < hs.nf; f++) {
@@ -667,7 +804,7 @@ void device_release(rt_scene* s) {
   if (s->device == RT_DEVICE_NONE) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
-  void* bufs[] = {s->d_nodes, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats,
+  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats,
                   s->d_rgb, s->d_face, s->d_t, s->d_hits};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -688,6 +825,9 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.mats = s->d_mats;
   P.sc.root = hs.root;
   P.sc.n_nodes = (int32_t)hs.nodes.size();
+  P.sc.nodes4 = s->d_nodes4;
+  P.sc.root4 = 0;
+  P.sc.n_nodes4 = (int32_t)hs.nodes4.size();
   memcpy(P.sc.Minv, hs.Minv, 64);
   memcpy(P.Minv, hs.Minv, 64);
   memcpy(P.MS, hs.MS, 36);
@@ -713,16 +853,24 @@ static int ensure_fb(rt_scene* s, size_t npix) {
 }
 
 // variant bits (debug knob RT_KERNEL_VARIANT, for A/B measurements; 0 = the measured-best default):
-// 1 = lane-register (VGPR) stack instead of the LDS stack, 4 = XCD-aware tile order
+// 1 = binary nodes + lane-register (VGPR) stack, 2 = 4-wide quantised nodes (when the scene has
+// them), 4 = XCD-aware tile order. Default: binary nodes + LDS stack.
+static int pick_trav(const FrameParams& P, int variant) {
+  if (variant & 1) return TRAV_B2_VGPR;
+  if ((variant & 2) && P.sc.n_nodes4 > 0) return TRAV_W4;
+  return TRAV_B2_LDS;
+}
 template <bool STATS>
-static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int variant) {
-  if (variant & 1) hipLaunchKernelGGL((k_trace_primary<STATS, false>), dim3(grid), dim3(256), 0, st, P);
-  else hipLaunchKernelGGL((k_trace_primary<STATS, true>), dim3(grid), dim3(256), 0, st, P);
+static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int trav) {
+  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_B2_VGPR>), dim3(grid), dim3(256), 0, st, P);
+  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_W4>), dim3(grid), dim3(256), 0, st, P);
 }
 template <bool STATS, bool HITS>
-static void launch_full(const FrameParams& P, int grid, hipStream_t st, int variant) {
-  if (variant & 1) hipLaunchKernelGGL((k_render_full<STATS, HITS, false>), dim3(grid), dim3(256), 0, st, P);
-  else hipLaunchKernelGGL((k_render_full<STATS, HITS, true>), dim3(grid), dim3(256), 0, st, P);
+static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav) {
+  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_VGPR>), dim3(grid), dim3(256), 0, st, P);
+  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_W4>), dim3(grid), dim3(256), 0, st, P);
 }
 
 static int kernel_variant() {
@@ -811,6 +959,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
   P.xcd_remap = (variant & 4) ? 1 : 0;
+  const int trav = pick_trav(P, variant);
   if (s->ev_used + 3 > s->ev_pool.size()) {
     if (s->ev_pool.size() >= 3 * 2048) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }
     for (int k = 0; k < 3; k++) {
@@ -826,14 +975,14 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   HIPCHECK(hipEventRecord(ev_a, st));
   if (grid > 0) {
     if (fr->mode == RT_MODE_PRIMARY) {
-      if (stats) launch_trace<true>(P, grid, st, variant); else launch_trace<false>(P, grid, st, variant);
+      if (stats) launch_trace<true>(P, grid, st, trav); else launch_trace<false>(P, grid, st, trav);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));
       if (hits) hipLaunchKernelGGL(k_shade_primary<true>, dim3(grid), dim3(256), 0, st, P);
       else hipLaunchKernelGGL(k_shade_primary<false>, dim3(grid), dim3(256), 0, st, P);
     } else {
-      if (stats) { if (hits) launch_full<true, true>(P, grid, st, variant); else launch_full<true, false>(P, grid, st, variant); }
-      else { if (hits) launch_full<false, true>(P, grid, st, variant); else launch_full<false, false>(P, grid, st, variant); }
+      if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav); else launch_full<true, false>(P, grid, st, trav); }
+      else { if (hits) launch_full<false, true>(P, grid, st, trav); else launch_full<false, false>(P, grid, st, trav); }
       HIPCHECK(hipEventRecord(ev_m, st));
     }
     HIPCHECK(hipGetLastError());
@@ -951,8 +1100,13 @@ static int trace_rays(rt_scene* s, int32_t n, const float* o, const float* d, in
     if (P3) { HIPCHECK(hipMalloc((void**)&d_P, n3)); R.P = d_P; }
   }
   const int grid = (n + 255) / 256;
-  if (any) hipLaunchKernelGGL(k_rays<true>, dim3(grid), dim3(256), 0, st, P, R);
-  else hipLaunchKernelGGL(k_rays<false>, dim3(grid), dim3(256), 0, st, P, R);
+  if (pick_trav(P, kernel_variant()) == TRAV_W4) {
+    if (any) hipLaunchKernelGGL((k_rays<true, TRAV_W4>), dim3(grid), dim3(256), 0, st, P, R);
+    else hipLaunchKernelGGL((k_rays<false, TRAV_W4>), dim3(grid), dim3(256), 0, st, P, R);
+  } else {
+    if (any) hipLaunchKernelGGL((k_rays<true, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P, R);
+    else hipLaunchKernelGGL((k_rays<false, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P, R);
+  }
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(st));
   if (any) {

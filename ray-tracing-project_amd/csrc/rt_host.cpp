@@ -761,6 +761,118 @@ void build_bvh(HostScene& hs, int leaf_size) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// 4-wide collapse: each wide node takes a binary node's two children and keeps opening the interior
+// child with the largest surface area until it has four children (or only leaves remain). Child
+// boxes (already padded) are quantised outward to 8 bits on a per-node, per-axis power-of-two grid.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+struct WChild {
+  float lo[3], hi[3];
+  uint32_t h;
+};
+
+void child_box(const Node64& n, int c, WChild& w) {
+  if (c == 0) {
+    w.lo[0] = n.c0lx; w.hi[0] = n.c0hx; w.lo[1] = n.c0ly; w.hi[1] = n.c0hy; w.lo[2] = n.c0lz; w.hi[2] = n.c0hz;
+    w.h = n.child0;
+  } else {
+    w.lo[0] = n.c1lx; w.hi[0] = n.c1hx; w.lo[1] = n.c1ly; w.hi[1] = n.c1hy; w.lo[2] = n.c1lz; w.hi[2] = n.c1hz;
+    w.h = n.child1;
+  }
+}
+
+float warea(const WChild& w) {
+  float d[3];
+  for (int k = 0; k < 3; k++) d[k] = std::max(0.0f, w.hi[k] - w.lo[k]);
+  return d[0] * d[1] + d[1] * d[2] + d[2] * d[0];
+}
+
+void quantize(Node4Q& q, const WChild* ch, int n) {
+  float L[3] = {INFINITY, INFINITY, INFINITY}, U[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int c = 0; c < n; c++)
+    for (int k = 0; k < 3; k++) { L[k] = std::min(L[k], ch[c].lo[k]); U[k] = std::max(U[k], ch[c].hi[k]); }
+  uint8_t eb[3];
+  double scale[3];
+  for (int k = 0; k < 3; k++) {
+    const double ext = (double)U[k] - (double)L[k];
+    int e = -100;
+    if (ext > 0) {
+      e = (int)std::ceil(std::log2(ext / 255.0));
+      while (std::ldexp(255.0, e) < ext) e++;
+      e = std::max(e, -100);
+    }
+    eb[k] = (uint8_t)(e + 127);
+    scale[k] = std::ldexp(1.0, e);
+  }
+  q.ox = L[0]; q.oy = L[1]; q.oz = L[2];
+  q.ex = eb[0]; q.ey = eb[1]; q.ez = eb[2];
+  q.valid = 0;
+  uint32_t* ql[3] = {&q.qlx, &q.qly, &q.qlz};
+  uint32_t* qh[3] = {&q.qhx, &q.qhy, &q.qhz};
+  for (int k = 0; k < 3; k++) { *ql[k] = 0; *qh[k] = 0; }
+  const double org[3] = {q.ox, q.oy, q.oz};
+  for (int c = 0; c < 4; c++) {
+    if (c >= n) { q.child[c] = 0; continue; }
+    q.valid |= (uint8_t)(1u << c);
+    q.child[c] = ch[c].h;
+    for (int k = 0; k < 3; k++) {
+      double a = std::floor(((double)ch[c].lo[k] - org[k]) / scale[k]);
+      double b = std::ceil(((double)ch[c].hi[k] - org[k]) / scale[k]);
+      a = std::min(std::max(a, 0.0), 255.0);
+      b = std::min(std::max(b, 0.0), 255.0);
+      while (a > 0 && org[k] + a * scale[k] > (double)ch[c].lo[k]) a -= 1;
+      while (b < 255 && org[k] + b * scale[k] < (double)ch[c].hi[k]) b += 1;
+      *ql[k] |= (uint32_t)a << (8 * c);
+      *qh[k] |= (uint32_t)b << (8 * c);
+    }
+  }
+  q.pad0 = q.pad1 = 0;
+}
+
+uint32_t collapse(const std::vector<Node64>& bin, uint32_t n2, std::vector<Node4Q>& out, int depth, int& maxd) {
+  maxd = std::max(maxd, depth);
+  WChild ch[4];
+  int n = 2;
+  child_box(bin[n2], 0, ch[0]);
+  child_box(bin[n2], 1, ch[1]);
+  // drop the never-hit sentinel child of a single-leaf root (inverted box)
+  if (ch[1].lo[0] > ch[1].hi[0]) n = 1;
+  while (n < 4) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int c = 0; c < n; c++)
+      if (!is_leaf(ch[c].h) && warea(ch[c]) > ba) { ba = warea(ch[c]); best = c; }
+    if (best < 0) break;
+    const Node64& sub = bin[ch[best].h];
+    WChild a, b;
+    child_box(sub, 0, a);
+    child_box(sub, 1, b);
+    ch[best] = a;
+    ch[n++] = b;
+  }
+  const uint32_t me = (uint32_t)out.size();
+  out.emplace_back();
+  uint32_t handles[4];
+  for (int c = 0; c < n; c++)
+    handles[c] = is_leaf(ch[c].h) ? ch[c].h : collapse(bin, ch[c].h, out, depth + 1, maxd);
+  for (int c = 0; c < n; c++) ch[c].h = handles[c];
+  quantize(out[me], ch, n);
+  return me;
+}
+}  // namespace
+
+void build_bvh4(HostScene& hs) {
+  hs.nodes4.clear();
+  hs.depth4 = 0;
+  if (hs.nodes.empty()) return;
+  hs.nodes4.reserve(hs.nodes.size() / 2 + 1);
+  int maxd = 0;
+  collapse(hs.nodes, hs.root, hs.nodes4, 0, maxd);
+  hs.depth4 = maxd + 1;
+}
+// (the wide traversal pushes at most 3 entries per level and writes up to 3 slots past the top)
+
 }  // namespace rt
 
 // =====================================================================================================
@@ -820,6 +932,8 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   }
   rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
   rt::build_bvh(hs, leaf);
+  rt::build_bvh4(hs);
+  if (3 * hs.depth4 + 4 > rt::kStack4) hs.nodes4.clear();  // too deep for the wide stack: binary traversal
   if (hs.depth > rt::kMaxDepth + 2) {  // the wave stack holds 64 entries
     delete s;
     rt::set_error("BVH depth %d exceeds the traversal stack", hs.depth);
@@ -878,5 +992,98 @@ extern "C" int rt_debug_math_host(int32_t op, int32_t n, const float* in, float*
   if (op < 0 || op > 16 || n < 0 || !in || !out) { rt::set_error("rt_debug_math_host: bad op"); return RT_ERR_INVALID; }
   for (int32_t k = 0; k < n; k++)
     if (rt::debug_math_case(op, in + (size_t)k * in_len[op], out + (size_t)k * out_len[op])) return RT_ERR_INVALID;
+  return RT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Acceleration-structure validation (rt_debug_validate_bvh)
+// ---------------------------------------------------------------------------------------------------
+namespace {
+struct VBox {
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void add(const VBox& b) {
+    for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+  }
+  bool inside(const double* l, const double* h) const {
+    for (int k = 0; k < 3; k++)
+      if (lo[k] <= hi[k] && (lo[k] < l[k] || hi[k] > h[k])) return false;
+    return true;
+  }
+};
+
+struct Validator {
+  const rt::HostScene& hs;
+  std::vector<int> seen2, seen4;
+  int64_t bad = 0;
+  VBox leaf(uint32_t h, std::vector<int>& seen) {
+    VBox b;
+    for (uint32_t i = rt::leaf_first(h); i < rt::leaf_first(h) + rt::leaf_count(h); i++) {
+      if (i >= hs.tris.size()) { bad++; continue; }
+      seen[i]++;
+      const rt::TriRec64& t = hs.tris[i];
+      const float v[9] = {t.w0x, t.w0y, t.w0z, t.w1x, t.w1y, t.w1z, t.w2x, t.w2y, t.w2z};
+      for (int j = 0; j < 3; j++)
+        for (int k = 0; k < 3; k++) { b.lo[k] = std::min(b.lo[k], (double)v[3 * j + k]); b.hi[k] = std::max(b.hi[k], (double)v[3 * j + k]); }
+    }
+    return b;
+  }
+  VBox bin(uint32_t n, int d, int64_t& depth) {
+    depth = std::max<int64_t>(depth, d + 1);
+    const rt::Node64& nd = hs.nodes[n];
+    VBox all;
+    for (int c = 0; c < 2; c++) {
+      const uint32_t h = c ? nd.child1 : nd.child0;
+      if ((c ? nd.c1lx : nd.c0lx) > (c ? nd.c1hx : nd.c0hx)) continue;  // never-hit sentinel child
+      const VBox b = rt::is_leaf(h) ? leaf(h, seen2) : bin(h, d + 1, depth);
+      const double l[3] = {c ? nd.c1lx : nd.c0lx, c ? nd.c1ly : nd.c0ly, c ? nd.c1lz : nd.c0lz};
+      const double u[3] = {c ? nd.c1hx : nd.c0hx, c ? nd.c1hy : nd.c0hy, c ? nd.c1hz : nd.c0hz};
+      if (!b.inside(l, u)) bad++;
+      all.add(b);
+    }
+    return all;
+  }
+  VBox wide(uint32_t n, int d, int64_t& depth) {
+    depth = std::max<int64_t>(depth, d + 1);
+    const rt::Node4Q& nd = hs.nodes4[n];
+    const double org[3] = {nd.ox, nd.oy, nd.oz};
+    const uint8_t e[3] = {nd.ex, nd.ey, nd.ez};
+    const uint32_t ql[3] = {nd.qlx, nd.qly, nd.qlz}, qh[3] = {nd.qhx, nd.qhy, nd.qhz};
+    VBox all;
+    for (int c = 0; c < 4; c++) {
+      if (!((nd.valid >> c) & 1)) continue;
+      const uint32_t h = nd.child[c];
+      const VBox b = rt::is_leaf(h) ? leaf(h, seen4) : wide(h, d + 1, depth);
+      double l[3], u[3];
+      for (int k = 0; k < 3; k++) {
+        // the device's cell size: the float with biased exponent e (2^(e-127))
+        const double sc = std::ldexp(1.0, (int)e[k] - 127);
+        l[k] = org[k] + ((ql[k] >> (8 * c)) & 255u) * sc;
+        u[k] = org[k] + ((qh[k] >> (8 * c)) & 255u) * sc;
+      }
+      if (!b.inside(l, u)) bad++;
+      all.add(b);
+    }
+    return all;
+  }
+};
+}  // namespace
+
+extern "C" int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]) {
+  if (!s || !info) { rt::set_error("rt_debug_validate_bvh: null argument"); return RT_ERR_INVALID; }
+  const rt::HostScene& hs = s->hs;
+  Validator v{hs, std::vector<int>(hs.tris.size()), std::vector<int>(hs.tris.size())};
+  for (int k = 0; k < 7; k++) info[k] = 0;
+  info[0] = (int64_t)hs.nodes.size();
+  info[2] = (int64_t)hs.nodes4.size();
+  if (!hs.nodes.empty()) v.bin(hs.root, 0, info[1]);
+  if (!hs.nodes4.empty()) v.wide(0, 0, info[3]);
+  for (size_t i = 0; i < hs.tris.size(); i++) {
+    info[4] += v.seen2[i] == 1;
+    info[5] += v.seen4[i] == 1;
+  }
+  info[6] = v.bad;
+  const bool ok = v.bad == 0 && info[4] == (int64_t)hs.tris.size() &&
+                  (hs.nodes4.empty() || info[5] == (int64_t)hs.tris.size());
+  if (!ok) { rt::set_error("acceleration structure check failed (%lld violations)", (long long)v.bad); return RT_ERR_INVALID; }
   return RT_OK;
 }

@@ -47,6 +47,19 @@ struct alignas(16) Node64 {
 };
 static_assert(sizeof(Node64) == 64, "node record must be 64 bytes");
 
+// 4-wide node, one 64-B record: the four children's boxes quantised to 8 bits on a per-node grid
+// (origin + q * 2^e per axis, rounded outward -> conservative), plus the four child handles.
+struct alignas(16) Node4Q {
+  float ox, oy, oz;        // grid origin
+  uint8_t ex, ey, ez;      // biased exponents: cell size 2^(e-127) per axis
+  uint8_t valid;           // bit c: child c present
+  uint32_t qlx, qhx, qly, qhy, qlz, qhz;  // byte c = child c's low / high cell index per axis
+  uint32_t child[4];       // child handles (internal node index or leaf handle)
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(Node4Q) == 64, "wide node record must be 64 bytes");
+constexpr int kStack4 = 128;  // per-wave stack entries of the 4-wide traversal (needs 3 * depth4 + 4)
+
 struct alignas(16) TriRec64 {
   float nx, ny, nz, dist;  // face.normal.normalized(), facenormal.dot(vert0)  (flyscene.cpp:450,459)
   float w0x, w0y, w0z, w1x;
@@ -71,6 +84,9 @@ struct Light {
 // Device scene view (pointers stay wave-uniform: SGPRs)
 struct DevScene {
   const Node64* nodes;
+  const Node4Q* nodes4;
+  uint32_t root4;
+  int32_t n_nodes4;
   const TriRec64* tris;
   const uint32_t* fshade;  // uint4 per face
   const float* vnorm;      // float4 per vertex

@@ -40,13 +40,15 @@ struct HostScene {
   std::vector<uint32_t> face_rank, face_box;
   // BVH
   std::vector<Node64> nodes;
+  std::vector<Node4Q> nodes4;  // 4-wide collapse of `nodes`
   std::vector<TriRec64> tris;  // leaf order
   uint32_t root = 0;
-  int32_t depth = 0, leaves = 0;
+  int32_t depth = 0, leaves = 0, depth4 = 0;
 };
 
 void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes);
 void build_bvh(HostScene& hs, int leaf_size);
+void build_bvh4(HostScene& hs);
 void set_error(const char* fmt, ...);
 
 }  // namespace rt
@@ -61,6 +63,7 @@ struct rt_scene {
   std::vector<void*> ev_pool;   // event pairs, one per render launch since the last synchronize
   size_t ev_used = 0;
   rt::Node64* d_nodes = nullptr;
+  rt::Node4Q* d_nodes4 = nullptr;
   rt::TriRec64* d_tris = nullptr;
   uint32_t* d_fshade = nullptr;
   float* d_vnorm = nullptr;
