@@ -204,6 +204,12 @@ const char* rt_last_error(void); /* thread-local */
 int rt_debug_math_host(int32_t op, int32_t n, const float* in, float* out);
 int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
 
+/* Host-side check of the scene's acceleration structures (tests only): every triangle lies inside
+ * each ancestor box of the binary tree and of the 4-wide quantised tree, and every triangle record
+ * sits in exactly one leaf of each. info[0..6] = binary nodes, binary depth, wide nodes, wide depth,
+ * triangles reached (binary), triangles reached (wide), containment violations. RT_OK iff sound. */
+int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,7 @@ EXPORTS = [
     "rt_write_ppm", "rt_scene_opts_default", "rt_scene_create", "rt_scene_destroy", "rt_scene_get_info",
     "rt_scene_ref_boxes", "rt_camera_flycam", "rt_render", "rt_render_async", "rt_synchronize",
     "rt_frame_download", "rt_trace_closest", "rt_trace_shadow", "rt_device_count", "rt_version",
-    "rt_last_error", "rt_debug_math_host", "rt_debug_math_device",
+    "rt_last_error", "rt_debug_math_host", "rt_debug_math_device", "rt_debug_validate_bvh",
 ]
 
 
@@ -109,6 +109,7 @@ def lib():
         L.rt_trace_shadow.argtypes = [vp, C.c_int32, vp, vp, vp]
         L.rt_debug_math_host.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_math_device.argtypes = [C.c_int32, C.c_int32, vp, vp]
+        L.rt_debug_validate_bvh.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -218,6 +219,15 @@ class Scene:
         i = SceneInfo()
         check(lib().rt_scene_get_info(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in i._fields_}
+
+    def validate_bvh(self):
+        """Host check of both trees (containment + exact leaf cover); returns the info counters."""
+        info = np.zeros(7, np.int64)
+        rc = lib().rt_debug_validate_bvh(self.h, _p(info))
+        keys = ["nodes2", "depth2", "nodes4", "depth4", "covered2", "covered4", "violations"]
+        out = dict(zip(keys, (int(x) for x in info)))
+        out["ok"] = rc == 0
+        return out
 
     def ref_boxes(self):
         inf = self.info()

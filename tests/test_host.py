@@ -109,6 +109,43 @@ def test_bvh_bounds_sane_for_empty_and_single(rt):
     assert info["n_faces"] == 0 and info["bvh_nodes"] == 0
 
 
+def _soup(rt, n, seed=3, scale=1.0, flat_axis=None):
+    v = rt.generate_soup(n, seed) * np.float32(scale)
+    if flat_axis is not None:
+        v[:, flat_axis] = np.float32(0.25 * scale)
+    return rt.Mesh.from_arrays(v, np.arange(3 * n, dtype=np.uint32).reshape(-1, 3),
+                               np.array([rt.SOUP_MATERIAL], np.float32))
+
+
+@pytest.mark.parametrize("case", ["cube", "dodgeColorTest", "bunny", "soup200k", "flat", "tiny", "huge",
+                                  "coincident", "single", "two"])
+def test_bvh_trees_sound(rt, case):
+    """Binary and 4-wide trees: every triangle inside every ancestor box (the wide boxes dequantised
+    exactly as the kernel does), every triangle record in exactly one leaf; depth fits the stacks."""
+    if case in ("cube", "dodgeColorTest", "bunny"):
+        mesh = rt.Mesh.load_obj(scene_path(case + ".obj"))
+    elif case == "soup200k":
+        mesh = _soup(rt, 200_000)
+    elif case == "flat":
+        mesh = _soup(rt, 20_000, flat_axis=2)
+    elif case == "tiny":
+        mesh = _soup(rt, 20_000, scale=1e-6)
+    elif case == "huge":
+        mesh = _soup(rt, 20_000, scale=1e6)
+    elif case == "coincident":
+        v = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (500, 1))
+        mesh = rt.Mesh.from_arrays(v, np.arange(1500, dtype=np.uint32).reshape(-1, 3),
+                                   np.array([rt.SOUP_MATERIAL], np.float32))
+    else:
+        mesh = _soup(rt, 1 if case == "single" else 2)
+    sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
+    r = sc.validate_bvh()
+    assert r["ok"] and r["violations"] == 0, r
+    nf = sc.info()["n_faces"]
+    assert r["covered2"] == nf and r["covered4"] == nf
+    assert r["nodes4"] >= 1 and r["depth4"] <= r["depth2"] and 3 * r["depth4"] + 4 <= 128
+
+
 def test_ppm_writer_format(rt, tmp_path):
     rgb = np.array([[[0.0, 0.5, 1.0], [1.5, -0.25, 0.999]]], np.float32)
     p = tmp_path / "x.ppm"
