@@ -1,12 +1,13 @@
 # Top-level build: the product library (gfx950 HIP + host C++) and the test oracle.
 #   make            -> ray-tracing-project_amd/lib/librtamd.so, oracle/build/liboracle.so, CLI
 # Float semantics: -ffp-contract=off everywhere (no FMA contraction; the reference rounds every op),
-# hipcc's default correctly rounded fp32 division / sqrt kept, no fast-math.
+# hipcc's default correctly rounded fp32 division / sqrt kept, no fast-math. -fno-slp-vectorize: the
+# SLP packing into v_pk_*_f32 costs more in lane shuffles than it saves here (measured -6% trace time).
 PKG      := ray-tracing-project_amd
 HIPCC    ?= /opt/rocm/bin/hipcc
 CXX      ?= g++
 ARCH     ?= gfx950
-HIPFLAGS := -O3 --offload-arch=$(ARCH) -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+HIPFLAGS := -O3 --offload-arch=$(ARCH) -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
             -munsafe-fp-atomics -Wall -Wno-unused-function -Wno-unused-variable
 CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 OBJ      := $(PKG)/build
@@ -27,6 +28,13 @@ $(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o
 	@mkdir -p $(PKG)/lib
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
+# A/B builds of the same sources with extra device flags (experiments only):
+#   make ablib TAG=noslp EXTRA="-fno-slp-vectorize"  ->  lib/librtamd_noslp.so  (select with RTAMD_LIB)
+ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o
+	@mkdir -p $(OBJ) $(PKG)/lib
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $(OBJ)/rt_device_$(TAG).o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_host.o -lpthread
+
 cli: $(PKG)/lib/rt_render_cli
 
 $(PKG)/lib/rt_render_cli: $(PKG)/host/main.cpp $(PKG)/host/flyscene.cpp $(PKG)/host/flyscene.hpp $(LIB)
@@ -45,4 +53,4 @@ clean:
 	rm -rf $(OBJ) $(PKG)/lib
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cli asm clean
+.PHONY: ablib all oracle cli asm clean

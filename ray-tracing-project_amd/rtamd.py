@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "librtamd.so")
+# RTAMD_LIB: an A/B build of the same library (`make ablib`), for measurements only
+LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(HERE, "lib", "librtamd.so")
 
 RT_MODE_PRIMARY = 0
 RT_MODE_FULL = 1
