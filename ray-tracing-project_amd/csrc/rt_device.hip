@@ -51,9 +51,9 @@ typedef int i16v __attribute__((ext_vector_type(16)));
 template <typename T>
 __device__ __forceinline__ T sload64(const T* base, uint32_t i) {
   static_assert(sizeof(T) == 64, "64-byte records");
-  const T* p = base + __builtin_amdgcn_readfirstlane(i);
+  const uint32_t off = __builtin_amdgcn_readfirstlane(i) * 64u;  // byte offset in an SGPR (< 4 GiB)
   i16v v;
-  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off) : "memory");
   T r;
   __builtin_memcpy(&r, &v, 64);
   return r;
@@ -209,7 +209,10 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
   uint64_t act = ballot(active);  // lanes still tracing (wave-uniform mask)
+  // one pop site and branch-free pushes keep the per-node control flow to the two uniform branches
+  // (interior vs leaf, pop vs descend)
   for (;;) {
+    bool pop = true;
     if (!is_leaf(node)) {
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
       if (STATS) {
@@ -220,51 +223,46 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       const Span s0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
       const Span s1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
       const uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
-      if ((m0 | m1) == 0) {  // no lane needs either child
-        if (sp == 0) break;
-        sp--;
-        node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
-        if (STATS) want = (flagstack >> sp) & 1;
-        continue;
-      }
-      // near child first by lane majority: each lane that needs a child votes for the one it enters first
+      // near child first by lane majority: each lane that needs a child votes for the one it enters
+      // first (covers m0 == 0 -> child 1 and m1 == 0 -> child 0)
       const uint64_t v0 = m0 & (~m1 | mask_le(s0.tmin, s1.tmin));
-      const bool first0 = (m1 == 0) | ((m0 != 0) & (2 * __popcll(v0) >= __popcll(m0 | m1)));
-      const uint32_t near = first0 ? nd.child0 : nd.child1;
-      const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
-      if ((m0 != 0) & (m1 != 0)) {
-        const uint32_t far = first0 ? nd.child1 : nd.child0;
-        if (STACK_LDS) lds_stack[sp] = far;
-        else stackv = (lane_id() == sp) ? far : stackv;  // v_cmp + v_cndmask
-        if (STATS) {
-          const bool wf = first0 ? h1 : h0;
-          flagstack = (flagstack & ~(1ull << sp)) | ((uint64_t)wf << sp);
-        }
-        sp++;
+      const bool first0 = 2 * __popcll(v0) >= __popcll(m0 | m1);
+      const uint32_t far = first0 ? nd.child1 : nd.child0;
+      // the far child is written above the top unconditionally and kept only when both are needed
+      if (STACK_LDS) lds_stack[sp] = far;
+      else stackv = (lane_id() == sp) ? far : stackv;  // v_cmp + v_cndmask
+      if (STATS) {
+        const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
+        const bool wf = first0 ? h1 : h0;
+        flagstack = (flagstack & ~(1ull << sp)) | ((uint64_t)wf << sp);
+        want = first0 ? h0 : h1;
       }
-      if (STATS) want = first0 ? h0 : h1;
-      node = near;
-      continue;
+      sp += ((m0 != 0) & (m1 != 0)) ? 1 : 0;
+      node = first0 ? nd.child0 : nd.child1;
+      pop = (m0 | m1) == 0;
+    } else {
+      // leaf: its triangles are fetched once per wave and tested by every lane
+      const uint32_t first = leaf_first(node), count = leaf_count(node);
+      if (STATS) {
+        if (want) cnt[ST_TRI] += count;
+        cnt[ST_WTRI] += count;
+      }
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = sload_tri(P.tris, first + k);
+        test_tri<ANY>(P, tr, first + k, r, active, h, found);
+      }
+      if (ANY) {
+        active = active & !found;
+        act = ballot(active);
+        if (!act) break;
+      }
     }
-    // leaf: its triangles are fetched once per wave and tested by every lane
-    const uint32_t first = leaf_first(node), count = leaf_count(node);
-    if (STATS) {
-      if (want) cnt[ST_TRI] += count;
-      cnt[ST_WTRI] += count;
+    if (pop) {
+      if (sp == 0) break;
+      sp--;
+      node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
+      if (STATS) want = (flagstack >> sp) & 1;
     }
-    for (uint32_t k = 0; k < count; k++) {
-      const TriRec64 tr = sload_tri(P.tris, first + k);
-      test_tri<ANY>(P, tr, first + k, r, active, h, found);
-    }
-    if (ANY) {
-      active = active & !found;
-      act = ballot(active);
-      if (!act) break;
-    }
-    if (sp == 0) break;
-    sp--;
-    node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
-    if (STATS) want = (flagstack >> sp) & 1;
   }
 }
 
