@@ -127,10 +127,17 @@ __device__ __forceinline__ bool ref_box_test(const Ray& r, const float* bx) {
 
 __device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
 
+// Lane masks straight from the compares (llvm.amdgcn.fcmp / icmp predicates): candidate sets stay in
+// SGPR pairs and wave-level decisions are one s_cmp, with no bool materialisation in VGPRs
+constexpr int kFcmpOEQ = 1, kFcmpOGE = 3, kFcmpOLT = 4, kFcmpUNE = 14, kIcmpULT = 36;
+template <int PRED>
+__device__ __forceinline__ uint64_t fmask(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, PRED); }
+__device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 // Rare path of a candidate (uniform triangle): interpolated normal non-zero (calculateDistance's
 // norm()==0 check, flyscene.cpp:467) and the reference box predicate. All loads wave-uniform.
-__device__ __forceinline__ bool accept_candidate(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0, f3 a1,
-                                                f3 a2, f3 p, const Ray& r, bool cand) {
+__device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0,
+                                                    f3 a1, f3 a2, f3 p, const Ray& r, uint64_t cand) {
   if (!(tr.box & kSafeNormalBit)) {  // uniform branch: only faces the host could not certify
     const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
     const float area = norm(cross(e0, neg(e2))) / 2;
@@ -139,7 +146,7 @@ __device__ __forceinline__ bool accept_candidate(const DevScene& P, const TriRec
     const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs[1]);
     const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs[2]);
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
-    cand = cand & (norm(nn) != 0);
+    cand &= fmask<kFcmpUNE>(norm(nn), 0.0f);
   }
   // reference box predicate. Fast path: the object-space hit point lies inside the reference box
   // with a margin (1e-5 relative) far above the reference slab test's rounding, so the exact ray
@@ -154,32 +161,33 @@ __device__ __forceinline__ bool accept_candidate(const DevScene& P, const TriRec
     const float m = 1e-5f * ((hi[k] - lo[k]) + fabsf(lo[k]) + fabsf(hi[k]) + fabsf(os[k])) + 1e-30f;
     inside = inside & (xs[k] > lo[k] + m) & (xs[k] < hi[k] - m);
   }
-  if (!ballot(cand & !inside)) return cand;
-  return cand & (inside | ref_box_test(r, bx));
+  const uint64_t ins = ballot(inside);
+  if ((cand & ~ins) == 0) return cand;
+  return cand & (ins | ballot(ref_box_test(r, bx)));
 }
 
-// calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record.
-// CLOSEST: update (t, rank, slot) if 0 <= t < best (rank breaks ties as the reference's order does).
-// ANY:     any valid t >= 0 (shadow(), flyscene.cpp:519).
+// calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record, for the lanes of
+// `act`. CLOSEST: update (t, rank, slot) if 0 <= t < best (rank breaks ties as the reference's order
+// does). ANY: any valid t >= 0 (shadow(), flyscene.cpp:519).
 template <bool ANY>
 __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, uint32_t slot, const Ray& r,
-                                         bool active, Hit& h, bool& found) {
+                                         uint64_t act, Hit& h, bool& found) {
   const f3 n{tr.nx, tr.ny, tr.nz};
   const float dn = dot(n, r.d);                 // facenormal.dot(dir)
   const float orth = tr.dist - dot(r.o, n);     // distancePlane - origin.dot(facenormal)
   const float t = orth / dn;                    // / dir.dot(facenormal)  (same bits as dn)
-  // predicates combined with bitwise ops: no per-lane branches (exec-mask traffic is SALU work)
-  bool cand;
-  if (ANY) cand = active & (dn != 0.0f) & (t >= 0.0f);
-  else cand = active & (dn != 0.0f) & (t >= 0.0f) & (t < INFINITY) & ((t < h.t) | ((t == h.t) & (tr.rank < h.rank)));
-  if (!ballot(cand)) return;
+  uint64_t cand = act & fmask<kFcmpUNE>(dn, 0.0f) & fmask<kFcmpOGE>(t, 0.0f);
+  if (!ANY)
+    cand &= fmask<kFcmpOLT>(t, INFINITY) &
+            (fmask<kFcmpOLT>(t, h.t) | (fmask<kFcmpOEQ>(t, h.t) & __builtin_amdgcn_uicmp(tr.rank, h.rank, kIcmpULT)));
+  if (cand == 0) return;
   const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  cand = cand & !((dot(n, a0) < 0) | (dot(n, a1) < 0) | (dot(n, a2) < 0));
-  if (!ballot(cand)) return;
-  const bool acc = accept_candidate(P, tr, e0, e2, a0, a1, a2, p, r, cand);
+  cand &= ~ballot((dot(n, a0) < 0) | (dot(n, a1) < 0) | (dot(n, a2) < 0));
+  if (cand == 0) return;
+  const bool acc = lane_in(accept_candidate(P, tr, e0, e2, a0, a1, a2, p, r, cand));
   if (ANY) {
     found = found | acc;
   } else {
@@ -222,6 +230,17 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       const float tcut = ANY ? tmax_any : h.t;
       const Span s0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
       const Span s1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+#ifdef RT_EXPERIMENT_NODES_TWICE  // timing experiment only: the box tests once more on opaque copies
+      {
+        Ray r2 = r;
+        float tc2 = tcut;
+        asm volatile("" : "+v"(r2.id.x), "+v"(r2.id.y), "+v"(r2.id.z), "+v"(r2.oid.x), "+v"(r2.oid.y), "+v"(r2.oid.z), "+v"(tc2));
+        const Span q0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r2, tc2);
+        const Span q1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r2, tc2);
+        uint64_t mm = mask_le(q0.tmin, q0.tmax) | mask_le(q1.tmin, q1.tmax);
+        asm volatile("" ::"s"(mm));
+      }
+#endif
       const uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
       // near child first by lane majority: each lane that needs a child votes for the one it enters
       // first (covers m0 == 0 -> child 1 and m1 == 0 -> child 0)
@@ -249,8 +268,14 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       }
       for (uint32_t k = 0; k < count; k++) {
         const TriRec64 tr = sload_tri(P.tris, first + k);
-        test_tri<ANY>(P, tr, first + k, r, active, h, found);
+        test_tri<ANY>(P, tr, first + k, r, act, h, found);
       }
+#ifdef RT_EXPERIMENT_TRIS_TWICE  // timing experiment only: the same leaf tested again (no effect)
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = sload_tri(P.tris, first + k);
+        test_tri<ANY>(P, tr, first + k, r, act, h, found);
+      }
+#endif
       if (ANY) {
         active = active & !found;
         act = ballot(active);
@@ -375,7 +400,7 @@ __device__ __forceinline__ void traverse4(const DevScene& P, const Ray& r, bool 
     }
     for (uint32_t q = 0; q < count; q++) {
       const TriRec64 tr = sload_tri(P.tris, first + q);
-      test_tri<ANY>(P, tr, first + q, r, active, h, found);
+      test_tri<ANY>(P, tr, first + q, r, act, h, found);
     }
     if (ANY) {
       active = active & !found;
@@ -512,7 +537,7 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   c.wv = (int)uniform(threadIdx.x >> 6);
   const int nb = (int)gridDim.x, b = (int)blockIdx.x;
   int L = b;
-  if (P.xcd_remap) {
+  if (P.xcd_remap == 1) {
     const int q = nb >> 3, rr = nb & 7, x = b & 7, k = b >> 3;
     L = x < rr ? x * (q + 1) + k : rr * (q + 1) + (x - rr) * q + k;
   }
@@ -856,7 +881,7 @@ static int ensure_fb(rt_scene* s, size_t npix) {
 
 // variant bits (debug knob RT_KERNEL_VARIANT, for A/B measurements; 0 = the measured-best default):
 // 1 = binary nodes + lane-register (VGPR) stack, 2 = 4-wide quantised nodes (when the scene has
-// them), 4 = XCD-aware tile order. Default: binary nodes + LDS stack.
+// them), 4 = XCD-contiguous tile order. Default: binary nodes + LDS stack.
 static int pick_trav(const FrameParams& P, int variant) {
   if (variant & 1) return TRAV_B2_VGPR;
   if ((variant & 2) && P.sc.n_nodes4 > 0) return TRAV_W4;

@@ -544,7 +544,8 @@ struct BvhBuilder {
   float pad;
   std::atomic<int> max_depth{0}, leaves{0};
   static constexpr int kBins = 32;
-  static constexpr float kTrav = 1.0f, kIsect = 1.0f;
+  static constexpr float kIsect = 1.0f;
+  float kTrav = 1.0f;  // node-visit cost relative to one triangle test (RT_SAH_TRAV, A/B knob)
 
   void set_child(Node64& n, int which, const Aabb& b, uint32_t h) const {
     float lo[3], hi[3];
@@ -705,6 +706,7 @@ void build_bvh(HostScene& hs, int leaf_size) {
   std::vector<Node64> tmp((size_t)std::max(hs.nf, 1));
   BvhBuilder B{prims, idx, tmp};
   B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
+  if (const char* e = getenv("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
   B.pad = pad;
   Aabb rootb;
   uint32_t root = B.build(0, (uint32_t)hs.nf, 0, rootb);
