@@ -48,22 +48,27 @@ def frame_for(n_gpus, override):
     return 8 * round(1920 * s / 8), 8 * round(1080 * s / 8), "weak"
 
 
-def cpu_baseline(rt_soup_args, W, H, target_s, threads):
+def cpu_baseline(scene, soup_args, W, H, full, target_s, threads):
     """Oracle ("port" of the reference algorithm) on a strided pixel sample of the same frame."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    n_tris, seed, mat = rt_soup_args
-    v = O.generate_soup(n_tris, seed)
-    f = np.arange(3 * n_tris, dtype=np.uint32).reshape(-1, 3)
     t0 = time.perf_counter()
-    sc = O.Scene(O.Mesh.from_arrays(v, f, np.array([mat], np.float32)))
+    if scene == "soup":
+        n_tris, seed, mat = soup_args
+        v = O.generate_soup(n_tris, seed)
+        f = np.arange(3 * n_tris, dtype=np.uint32).reshape(-1, 3)
+        sc = O.Scene(O.Mesh.from_arrays(v, f, np.array([mat], np.float32)))
+        what = f"{n_tris}-tri soup"
+    else:
+        sc = O.Scene(O.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj")))
+        what = "bunny"
     build_s = time.perf_counter() - t0
     cam = O.flycam(W, H, 0, 0, 20)
 
     def run(step):
         pix = np.array([(i, j) for j in range(step // 2, H, step) for i in range(step // 3, W, step)], np.int32)
         t = time.perf_counter()
-        sc.render(cam, O.DEFAULT_LIGHTS, W, H, full=False, pixels=pix, threads=threads)
+        sc.render(cam, O.DEFAULT_LIGHTS, W, H, full=full, pixels=pix, threads=threads)
         return len(pix), time.perf_counter() - t
 
     n, dt = run(23)  # calibration sample (~4k rays)
@@ -75,8 +80,8 @@ def cpu_baseline(rt_soup_args, W, H, target_s, threads):
             break
     return {"value": round(n / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{n} primary rays = every {step}th pixel in x and y of the same {W}x{H} frame "
-                      f"(1M-tri scene, eye (0,0,1)); {dt:.1f} s of CPU work on {threads} threads; "
-                      f"box partition build {build_s:.1f} s excluded"}
+                      f"({what}, eye (0,0,1), {'FULL' if full else 'PRIMARY'}); {dt:.1f} s of CPU work on "
+                      f"{threads} threads; box partition build {build_s:.1f} s excluded"}
 
 
 def shard_tiles(W, H, rank, n):
@@ -225,10 +230,19 @@ def main():
     cpu = None
     if rank == 0 and n == 1 and not a.no_cpu:
         threads = min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline((a.tris, 12345, rt.SOUP_MATERIAL), W, H, a.cpu_seconds, threads)
+        cpu = cpu_baseline(a.scene, (a.tris, 12345, rt.SOUP_MATERIAL), W, H, a.mode == "full", a.cpu_seconds,
+                           threads)
 
     if rank == 0:
         value = total_rays / elapsed_max / 1e6
+        if a.scene == "soup":
+            cname = "C3" if (W, H) == (1920, 1080) else ("C4" if (W, H) == (3840, 2160) else "C3-family")
+        else:
+            cname = "C5" if a.mode == "full" else "C2"
+        extra = {}
+        if stats is not None:
+            extra["rays_per_frame_total"] = stats["total_rays"]  # primary + shadow + reflection (FULL)
+            extra["total_mrays_per_s"] = round(stats["total_rays"] * n * a.steps / elapsed_max / 1e6, 2)
         out = {
             "metric": "Mrays/s (primary) + frame ms at 1920x1080, 1M-tri BVH, 1/2/4/8 GPU",
             "value": round(value, 2),
@@ -242,14 +256,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"C3: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light",
+            "config": {"workload": f"{cname}: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light",
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
                        "parallelism": f"tiles/{n} (16x16 tiles interleaved over ranks, scene replicated)",
                        "kernel_ms_per_frame": round(kernel_ms_max, 4),
                        "trace_kernel_ms": round(trace_ms_max, 4),
                        "kernel_mrays_per_s": round(total_rays / a.steps / (kernel_ms_max * 1e-3) / 1e6, 2),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
-                       "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2)},
+                       "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2), **extra},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
