@@ -17,7 +17,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_trace_primary<false, 2>"):
+def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_trace_primary<false, 1>"):
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     stats_src = os.path.join(prof, "trace", "run_kernel_stats.csv")
     shutil.copy(stats_src, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
