@@ -210,6 +210,13 @@ int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
  * triangles reached (binary), triangles reached (wide), containment violations. RT_OK iff sound. */
 int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]);
 
+/* Kernel-variant override (tests and A/B measurements only; default 0 = the measured-best kernels):
+ * same bits as the RT_KERNEL_VARIANT environment variable (1 VGPR wave stack, 2 4-wide quantised
+ * BVH, 4 XCD-contiguous tile order, 16 FULL as a stage pipeline, +32/64/128 per-lane traversal in
+ * its reflection / secondary-shadow / primary-shadow stages). Every variant renders the same bits.
+ * Returns the previous value. */
+int rt_debug_set_variant(int32_t v);
+
 #ifdef __cplusplus
 }
 #endif

@@ -414,13 +414,128 @@ __device__ __forceinline__ void traverse4(const DevScene& P, const Ray& r, bool 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Per-lane traversal for incoherent rays (reflection and secondary shadow rays): every lane walks its
+// own path with its own stack ("while-while": descend interior nodes until every lane holds a leaf or
+// is done, then test leaves). Node and triangle records are per-lane vector loads. The triangle test
+// is the same arithmetic as test_tri, per lane, so results are identical.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T vload64(const T* base, uint32_t i) {
+  static_assert(sizeof(T) == 64, "64-byte records");
+  const float4* p = reinterpret_cast<const float4*>(base + i);
+  T r;
+  float4* q = reinterpret_cast<float4*>(&r);
+  q[0] = p[0]; q[1] = p[1]; q[2] = p[2]; q[3] = p[3];
+  return r;
+}
+
+// the rare accept path of one lane (accept_candidate, per lane)
+__device__ __forceinline__ bool accept_lane(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0, f3 a1, f3 a2,
+                                            f3 p, const Ray& r) {
+  if (!(tr.box & kSafeNormalBit)) {
+    const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
+    const float area = norm(cross(e0, neg(e2))) / 2;
+    const uint4 fs = *reinterpret_cast<const uint4*>(P.fshade + 4 * (size_t)tr.face);
+    const f3 n0 = ld3(P.vnorm + 4 * (size_t)fs.x);
+    const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs.y);
+    const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs.z);
+    const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
+    if (!(norm(nn) != 0)) return false;
+  }
+  const float* bx = P.refbox + 8 * (size_t)(tr.box & ~kSafeNormalBit);
+  const f3 X = affv3(P.Minv, p);
+  const float lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[4], bx[5], bx[6]};
+  const float xs[3] = {X.x, X.y, X.z}, os[3] = {r.o2.x, r.o2.y, r.o2.z};
+  bool inside = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float m = 1e-5f * ((hi[k] - lo[k]) + fabsf(lo[k]) + fabsf(hi[k]) + fabsf(os[k])) + 1e-30f;
+    inside = inside & (xs[k] > lo[k] + m) & (xs[k] < hi[k] - m);
+  }
+  return inside || ref_box_test(r, bx);
+}
+
+// calculateDistance (flyscene.cpp:444-478) of one lane against its own triangle record
+template <bool ANY>
+__device__ __forceinline__ void test_tri_lane(const DevScene& P, const TriRec64& tr, uint32_t slot, const Ray& r,
+                                              Hit& h, bool& found) {
+  const f3 n{tr.nx, tr.ny, tr.nz};
+  const float dn = dot(n, r.d);
+  const float orth = tr.dist - dot(r.o, n);
+  const float t = orth / dn;
+  bool cand = (dn != 0.0f) & (t >= 0.0f);
+  if (!ANY) cand = cand & (t < INFINITY) & ((t < h.t) | ((t == h.t) & (tr.rank < h.rank)));
+  if (!cand) return;
+  const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
+  const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
+  const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
+  const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
+  if ((dot(n, a0) < 0) | (dot(n, a1) < 0) | (dot(n, a2) < 0)) return;
+  if (!accept_lane(P, tr, e0, e2, a0, a1, a2, p, r)) return;
+  if (ANY) {
+    found = true;
+  } else {
+    h.t = t;
+    h.rank = tr.rank;
+    h.slot = slot;
+  }
+}
+
+constexpr int kLaneStack = kMaxDepth + 4;
+
+template <bool ANY, bool STATS>
+__device__ __forceinline__ void traverse_lane(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                              uint32_t* cnt) {
+  if (P.n_nodes == 0) return;
+  uint32_t stack[kLaneStack];  // per-lane stack (private memory)
+  int sp = 0;
+  uint32_t node = P.root;
+  bool done = !active;
+  for (;;) {
+    // descend interior nodes until this lane holds a leaf or has nothing left
+    while (!done && !is_leaf(node)) {
+      const Node64 nd = vload64(P.nodes, node);
+      if (STATS) cnt[ST_NODE]++;
+      const float tcut = ANY ? INFINITY : h.t;
+      const Span s0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
+      const Span s1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+      const bool h0 = s0.tmin <= s0.tmax, h1 = s1.tmin <= s1.tmax;
+      if (h0 && h1) {
+        const bool first0 = s0.tmin <= s1.tmin;
+        stack[sp++] = first0 ? nd.child1 : nd.child0;
+        node = first0 ? nd.child0 : nd.child1;
+      } else if (h0 | h1) {
+        node = h0 ? nd.child0 : nd.child1;
+      } else if (sp > 0) {
+        node = stack[--sp];
+      } else {
+        done = true;
+      }
+    }
+    if (!done) {
+      const uint32_t first = leaf_first(node), count = leaf_count(node);
+      if (STATS) cnt[ST_TRI] += count;
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = vload64(P.tris, first + k);
+        test_tri_lane<ANY>(P, tr, first + k, r, h, found);
+        if (ANY && found) break;
+      }
+      if (ANY && found) done = true;
+      else if (sp > 0) node = stack[--sp];
+      else done = true;
+    }
+    if (ballot(!done) == 0) break;
+  }
+}
+
 // Traversal flavours (A/B knob RT_KERNEL_VARIANT): binary nodes with the VGPR or the LDS stack, or
 // the 4-wide quantised nodes
-enum { TRAV_B2_VGPR = 0, TRAV_B2_LDS = 1, TRAV_W4 = 2 };
+enum { TRAV_B2_VGPR = 0, TRAV_B2_LDS = 1, TRAV_W4 = 2, TRAV_LANE = 3 };
 
 template <int TRAV, bool STATS>
 struct WaveLds {
-  static constexpr int kEntries = TRAV == TRAV_W4 ? kStack4 : 64;
+  static constexpr int kEntries = TRAV == TRAV_W4 ? kStack4 : (TRAV == TRAV_LANE ? 1 : 64);
   uint32_t stack[4][kEntries];
   uint64_t mask[4][(STATS && TRAV == TRAV_W4) ? kEntries : 1];
 };
@@ -429,6 +544,7 @@ template <bool ANY, bool STATS, int TRAV>
 __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                       WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   if (TRAV == TRAV_W4) traverse4<ANY, STATS>(P, r, active, h, found, L.stack[wv], L.mask[STATS ? wv : 0], cnt);
+  else if (TRAV == TRAV_LANE) traverse_lane<ANY, STATS>(P, r, active, h, found, cnt);
   else traverse<ANY, STATS, TRAV == TRAV_B2_LDS>(P, r, active, h, found, L.stack[wv], cnt);
 }
 
@@ -592,6 +708,10 @@ void k_trace_primary(FrameParams P) {
   trace<false, STATS, TRAV>(P.sc, r, c.active, h, dummy, lds, c.wv, cnt);
   if (STATS && c.active && h.t != INFINITY) cnt[ST_HITS]++;
   if (c.active) P.hits[(size_t)c.py * P.W + c.px] = make_uint2(__float_as_uint(h.t), h.slot);
+  if (P.wcount0 != nullptr) {  // FULL pipeline: per-wave hit count for the list0 compaction
+    const uint32_t nh = (uint32_t)__popcll(ballot(c.active && h.t != INFINITY));
+    if (c.lane == 0) P.wcount0[blockIdx.x * 4 + c.wv] = nh;
+  }
   if (STATS) flush_stats(P, cnt, c.lane);
 }
 
@@ -634,8 +754,12 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
 
 // FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
 // bounce, all in one kernel (flyscene.cpp:317-371, 510-566, 603-614).
+#ifndef RT_FULL_WAVES_PER_EU
+#define RT_FULL_WAVES_PER_EU 8  // measured: 8 waves (64 VGPR + stack spill) beats 3 (150 VGPR) by 24% on C3 FULL
+#endif
 template <bool STATS, bool HITS, int TRAV>
-__global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU)))
+void k_render_full(FrameParams P) {
   __shared__ WaveLds<TRAV, STATS> lds;
   const PixelCoord c = pixel_coord(P);
   const bool active = c.active;
@@ -711,6 +835,263 @@ __global__ __launch_bounds__(256) void k_render_full(FrameParams P) {
     }
   }
   if (STATS) flush_stats(P, cnt, c.lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+// FULL as a wavefront pipeline: k_render_full's work cut at every traversal into lean stage kernels
+// (each at full occupancy) that hand per-pixel records through HBM:
+//   k_trace_primary -> k_full_gen0 -> k_full_shadow(0) -> k_full_refl -> k_full_gen1 -> k_full_shadow(1)
+//   -> k_full_final
+// Same expressions and the same order of sticky material updates as the megakernel, so the frame is
+// bit-identical to it (and to the oracle's traceRay).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ HitState no_hit_state() {
+  HitState h;
+  h.px = h.py = h.pz = 0.0f;
+  h.nx = h.ny = h.nz = 0.0f;
+  h.mat = -1;
+  h.face = 0xFFFFFFFFu;
+  return h;
+}
+__device__ __forceinline__ HitState to_state(const HitInfo& hi) {
+  HitState h;
+  h.px = hi.p.x; h.py = hi.p.y; h.pz = hi.p.z;
+  h.nx = hi.n.x; h.ny = hi.n.y; h.nz = hi.n.z;
+  h.mat = hi.mat;
+  h.face = hi.face;
+  return h;
+}
+__device__ __forceinline__ HitInfo from_state(const HitState& h) {
+  HitInfo hi;
+  hi.p = f3{h.px, h.py, h.pz};
+  hi.n = f3{h.nx, h.ny, h.nz};
+  hi.mat = h.mat;
+  hi.face = h.face;
+  return hi;
+}
+__device__ __forceinline__ size_t pixel_index(const FrameParams& P, const PixelCoord& c) {
+  return (size_t)c.py * P.W + c.px;
+}
+
+// Compaction without atomics: each producer wave stores its count of selected lanes, one block
+// scans the counts (k_scan_counts), and the consumer of the next stage writes its selected lanes to
+// list[offset[wave] + rank among the wave's selected lanes]. The list is in wave order, so 64
+// consecutive entries come from neighbouring tiles and packets stay coherent.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// exclusive prefix sum of cnt[0..q) into off[], total into *total (one 1024-thread block)
+__global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* cnt, uint32_t* off, int q, uint32_t* total) {
+  __shared__ uint32_t part[1024];
+  const int t = (int)threadIdx.x;
+  const int per = (q + 1023) / 1024;
+  const int b = t * per, e = min(q, b + per);
+  uint32_t sum = 0;
+  for (int i = b; i < e; i++) sum += cnt[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (int i = b; i < e; i++) {
+    off[i] = run;
+    run += cnt[i];
+  }
+  if (t == 1023) *total = part[1023];
+}
+
+// list wave w of a list-consuming kernel: entries [64 w, 64 w + 64) of a list of n
+struct ListLane {
+  int w;          // list wave index (uniform)
+  uint32_t i;     // this lane's list position
+  bool act;       // i < n
+  bool any;       // the wave has at least one entry
+};
+__device__ __forceinline__ ListLane list_lane(uint32_t n) {
+  ListLane L;
+  L.w = (int)uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  L.i = (uint32_t)L.w * 64u + (uint32_t)lane_id();
+  L.act = L.i < n;
+  L.any = (uint32_t)L.w * 64u < n;
+  return L;
+}
+
+// primary hit record -> hit point, interpolated normal, material; and the reflection ray
+// (traceRay flyscene.cpp:336-363)
+__global__ __launch_bounds__(256) void k_full_gen0(FrameParams P) {
+  const PixelCoord c = pixel_coord(P);
+  const size_t pix = c.active ? pixel_index(P, c) : 0;
+  const float t = c.active ? __uint_as_float(P.hits[pix].x) : INFINITY;
+  // scatter this wave's hit pixels into list0 (offsets from the primary kernel's counts)
+  const uint64_t hm = ballot(t != INFINITY);
+  if (t != INFINITY) P.list0[P.woff0[blockIdx.x * 4 + c.wv] + lanes_below(hm)] = (uint32_t)pix;
+  if (!c.active) return;
+  const uint2 hb = P.hits[pix];
+  HitState hs = no_hit_state();
+  RayRec rq{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0u, 0u};
+  if (t != INFINITY) {
+    const Ray r = primary_ray(P, c.px, c.py);
+    const TriRec64 tr0 = vload_tri(P.sc.tris, hb.y);
+    HitInfo hi0;
+    hi0.face = tr0.face;
+    hi0.p = f3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
+    hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
+    hs = to_state(hi0);
+    const f3 d = reflect(normalized(r.d), hi0.n);
+    const f3 o = offset(hi0.p, d, 0.001f);
+    rq = RayRec{o.x, o.y, o.z, d.x, d.y, d.z, 0u, 0u};
+  }
+  P.state0[pix] = hs;
+  P.refl[pix] = rq;
+}
+
+// shadow() for every light from the hits listed for `pass` (0: primary, 1: reflection): per-light
+// blocked bits. One wave per 64 list entries.
+template <bool STATS, int TRAV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
+void k_full_shadow(FrameParams P, int pass) {
+  __shared__ WaveLds<TRAV, STATS> lds;
+  const ListLane L = list_lane(P.counters[pass]);
+  if (!L.any) return;
+  const int wv = (int)uniform(threadIdx.x >> 6);
+  const uint32_t pix = L.act ? (pass ? P.list1 : P.list0)[L.i] : 0u;
+  const HitState hs = (pass ? P.state1 : P.state0)[pix];
+  const f3 p{hs.px, hs.py, hs.pz};
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t bits = 0;
+  for (int l = 0; l < P.n_lights; l++) {
+    const float* lp = P.lights[l].p;
+    const f3 Ld = neg(normalized(sub(p, f3{lp[0], lp[1], lp[2]})));
+    Ray sr;
+    sr.o = offset(p, Ld, 0.003f);
+    sr.d = Ld;
+    sr.o2 = affv3(P.Minv, p);
+    sr.d2 = normalized(m3v3(P.MS, Ld));
+    setup_cull(sr);
+    Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    bool blocked = false;
+    if (STATS && L.act) cnt[ST_TOTAL]++;
+    trace<true, STATS, TRAV>(P.sc, sr, L.act, hh, blocked, lds, wv, cnt);
+    bits |= (blocked ? 1u : 0u) << l;
+  }
+  if (L.act) (pass ? P.blk1 : P.blk0)[pix] = bits;
+  if (STATS) flush_stats(P, cnt, lane_id());
+}
+
+// the reflection ray's closest hit (traceRay depth 1, flyscene.cpp:361-363) for the list0 pixels;
+// per list wave the number of reflection hits (list1 compaction)
+template <bool STATS, int TRAV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
+void k_full_refl(FrameParams P) {
+  __shared__ WaveLds<TRAV, STATS> lds;
+  const ListLane L = list_lane(P.counters[0]);
+  if (!L.any) {
+    if (L.w < P.n_waves_max && lane_id() == 0) P.wcount1[L.w] = 0;
+    return;
+  }
+  const int wv = (int)uniform(threadIdx.x >> 6);
+  const uint32_t pix = L.act ? P.list0[L.i] : 0u;
+  const RayRec rq = P.refl[pix];
+  Ray rr;
+  rr.d = f3{rq.dx, rq.dy, rq.dz};
+  rr.o = f3{rq.ox, rq.oy, rq.oz};
+  rr.o2 = affv3(P.Minv, rr.o);
+  rr.d2 = normalized(m3v3(P.MS, rr.d));
+  setup_cull(rr);
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  if (STATS && L.act) cnt[ST_TOTAL]++;
+  Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  bool dummy = false;
+  trace<false, STATS, TRAV>(P.sc, rr, L.act, h1, dummy, lds, wv, cnt);
+  if (L.act) P.hits1[pix] = make_uint2(__float_as_uint(h1.t), h1.slot);
+  const uint32_t nh = (uint32_t)__popcll(ballot(L.act && h1.t != INFINITY));
+  if (lane_id() == 0) P.wcount1[L.w] = nh;
+  if (STATS) flush_stats(P, cnt, lane_id());
+}
+
+// reflection hit record -> hit point, interpolated normal, material for every list0 pixel; scatters
+// the reflection-hit pixels into list1
+__global__ __launch_bounds__(256) void k_full_gen1(FrameParams P) {
+  const ListLane L = list_lane(P.counters[0]);
+  if (!L.any) return;
+  const uint32_t pix = L.act ? P.list0[L.i] : 0u;
+  const uint2 hb = P.hits1[pix];
+  const float t = L.act ? __uint_as_float(hb.x) : INFINITY;
+  const uint64_t hm = ballot(t != INFINITY);
+  if (t != INFINITY) P.list1[P.woff1[L.w] + lanes_below(hm)] = pix;
+  if (!L.act) return;
+  HitState hs = no_hit_state();
+  if (t != INFINITY) {
+    const RayRec rq = P.refl[pix];
+    const TriRec64 tr1 = vload_tri(P.sc.tris, hb.y);
+    HitInfo hi1;
+    hi1.face = tr1.face;
+    hi1.p = f3{rq.ox + t * rq.dx, rq.oy + t * rq.dy, rq.oz + t * rq.dz};
+    hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
+    hs = to_state(hi1);
+  }
+  P.state1[pix] = hs;
+}
+
+// calculateColor (flyscene.cpp:603-614) with the shadow() outcomes already known (bit l: light l blocked)
+__device__ __forceinline__ f3 calc_color_bits(const FrameParams& P, MatState& st, const HitInfo& hi, f3 o, bool lane_hit,
+                                              uint32_t bits) {
+  f3 sum{0.0f, 0.0f, 0.0f};
+  for (int l = 0; l < P.n_lights; l++) {
+    const float* lp = P.lights[l].p;
+    const f3 L = neg(normalized(sub(hi.p, f3{lp[0], lp[1], lp[2]})));
+    const bool blocked = (bits >> l) & 1u;
+    f3 c{0.0f, 0.0f, 0.0f};
+    if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
+    sum = f3{sum.x + c.x, sum.y + c.y, sum.z + c.z};
+  }
+  return f3{clamp01(sum.x), clamp01(sum.y), clamp01(sum.z)};
+}
+
+// traceRay's colour composition (flyscene.cpp:327-370), the megakernel's tail
+template <bool HITS>
+__global__ __launch_bounds__(256) void k_full_final(FrameParams P) {
+  const PixelCoord c = pixel_coord(P);
+  if (!c.active) return;
+  const size_t pix = pixel_index(P, c);
+  const HitState s0 = P.state0[pix];
+  const bool hit0 = s0.face != 0xFFFFFFFFu;
+  MatState st = load_mat(P.defmat);
+  const HitInfo hi0 = from_state(s0);
+  const f3 eye{P.eye[0], P.eye[1], P.eye[2]};
+  const f3 direct0 = calc_color_bits(P, st, hi0, eye, hit0, hit0 ? P.blk0[pix] : 0u);
+  if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
+  f3 refl{0.0f, 0.0f, 0.0f};
+  // state1 / refl / blk1 exist only for primary-hit pixels (and blk1 only for reflection hits)
+  const HitState s1 = hit0 ? P.state1[pix] : no_hit_state();
+  const bool hit1 = hit0 && s1.face != 0xFFFFFFFFu;
+  const HitInfo hi1 = from_state(s1);
+  const RayRec rq = hit0 ? P.refl[pix] : RayRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0u, 0u};
+  const f3 direct1 = calc_color_bits(P, st, hi1, f3{rq.ox, rq.oy, rq.oz}, hit1, hit1 ? P.blk1[pix] : 0u);
+  if (hit1) {
+    if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
+    refl = f3{clamp01(direct1.x + 0.0f * st.ks.x), clamp01(direct1.y + 0.0f * st.ks.y),
+              clamp01(direct1.z + 0.0f * st.ks.z)};
+  }
+  f3 col;
+  if (hit0) {
+    col = f3{clamp01(direct0.x + refl.x * st.ks.x), clamp01(direct0.y + refl.y * st.ks.y),
+             clamp01(direct0.z + refl.z * st.ks.z)};
+  } else {
+    col = f3{P.bg[0], P.bg[1], P.bg[2]};
+  }
+  P.rgb[3 * pix + 0] = col.x;
+  P.rgb[3 * pix + 1] = col.y;
+  P.rgb[3 * pix + 2] = col.z;
+  if (HITS) {
+    P.face_out[pix] = hit0 ? (int32_t)s0.face : -1;
+    P.t_out[pix] = __uint_as_float(P.hits[pix].x);
+  }
 }
 
 // Ray-list kernels (rt_trace_closest / rt_trace_shadow), 64 rays per wave
@@ -832,7 +1213,7 @@ void device_release(rt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
   void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats,
-                  s->d_rgb, s->d_face, s->d_t, s->d_hits};
+                  s->d_rgb, s->d_face, s->d_t, s->d_hits, s->d_full};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
@@ -864,6 +1245,40 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   memcpy(P.bg, s->opts.background, 12);
 }
 
+// FULL pipeline hand-off buffers: state0, state1 (32 B), refl (32 B), hits1 (8 B), blk0, blk1, list0,
+// list1 (4 B) per pixel; then per list wave wcount0/1, woff0/1; then the counters
+constexpr size_t kFullBytesPerPixel = 32 + 32 + 32 + 8 + 4 + 4 + 4 + 4;
+static size_t full_waves(size_t npix) { return (npix + 63) / 64 + 8; }
+static int ensure_full(rt_scene* s, size_t npix) {
+  if (npix <= s->full_pixels) return RT_OK;
+  if (s->d_full) (void)hipFree(s->d_full);
+  s->d_full = nullptr;
+  s->full_pixels = 0;
+  HIPCHECK(hipMalloc(&s->d_full, npix * kFullBytesPerPixel + 16 * full_waves(npix) + 64));
+  s->full_pixels = npix;
+  return RT_OK;
+}
+static void bind_full(const rt_scene* s, FrameParams& P) {
+  char* b = (char*)s->d_full;
+  const size_t n = s->full_pixels;
+  P.state0 = (HitState*)b;
+  P.state1 = (HitState*)(b + 32 * n);
+  P.refl = (RayRec*)(b + 64 * n);
+  P.hits1 = (uint2*)(b + 96 * n);
+  P.blk0 = (uint32_t*)(b + 104 * n);
+  P.blk1 = (uint32_t*)(b + 108 * n);
+  P.list0 = (uint32_t*)(b + 112 * n);
+  P.list1 = (uint32_t*)(b + 116 * n);
+  const size_t q = full_waves(n);
+  char* w = b + 120 * n;
+  P.wcount0 = (uint32_t*)w;
+  P.wcount1 = (uint32_t*)(w + 4 * q);
+  P.woff0 = (uint32_t*)(w + 8 * q);
+  P.woff1 = (uint32_t*)(w + 12 * q);
+  P.counters = (uint32_t*)(w + 16 * q);
+  P.n_waves_max = (int32_t)q;
+}
+
 static int ensure_fb(rt_scene* s, size_t npix) {
   if (npix <= s->fb_pixels) return RT_OK;
   if (s->d_rgb) (void)hipFree(s->d_rgb);
@@ -881,7 +1296,10 @@ static int ensure_fb(rt_scene* s, size_t npix) {
 
 // variant bits (debug knob RT_KERNEL_VARIANT, for A/B measurements; 0 = the measured-best default):
 // 1 = binary nodes + lane-register (VGPR) stack, 2 = 4-wide quantised nodes (when the scene has
-// them), 4 = XCD-contiguous tile order. Default: binary nodes + LDS stack.
+// them), 4 = XCD-contiguous tile order, 16 = FULL as the stage pipeline (k_full_*) instead of one
+// kernel; with 16: 32 / 64 / 128 = per-lane traversal for the reflection rays / the shadow rays of
+// reflection hits / the shadow rays of primary hits. Default: binary nodes + LDS stack, FULL as one
+// kernel (k_render_full).
 static int pick_trav(const FrameParams& P, int variant) {
   if (variant & 1) return TRAV_B2_VGPR;
   if ((variant & 2) && P.sc.n_nodes4 > 0) return TRAV_W4;
@@ -900,13 +1318,53 @@ static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav
   else hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_W4>), dim3(grid), dim3(256), 0, st, P);
 }
 
+template <bool STATS>
+static void launch_shadow(const FrameParams& P, int g, hipStream_t st, int trav, int pass) {
+  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_full_shadow<STATS, TRAV_B2_VGPR>), dim3(g), dim3(256), 0, st, P, pass);
+  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_full_shadow<STATS, TRAV_B2_LDS>), dim3(g), dim3(256), 0, st, P, pass);
+  else if (trav == TRAV_W4) hipLaunchKernelGGL((k_full_shadow<STATS, TRAV_W4>), dim3(g), dim3(256), 0, st, P, pass);
+  else hipLaunchKernelGGL((k_full_shadow<STATS, TRAV_LANE>), dim3(g), dim3(256), 0, st, P, pass);
+}
+template <bool STATS>
+static void launch_refl(const FrameParams& P, int g, hipStream_t st, int trav) {
+  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_full_refl<STATS, TRAV_B2_VGPR>), dim3(g), dim3(256), 0, st, P);
+  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_full_refl<STATS, TRAV_B2_LDS>), dim3(g), dim3(256), 0, st, P);
+  else if (trav == TRAV_W4) hipLaunchKernelGGL((k_full_refl<STATS, TRAV_W4>), dim3(g), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL((k_full_refl<STATS, TRAV_LANE>), dim3(g), dim3(256), 0, st, P);
+}
+
+// traversal per FULL stage: packets for the coherent primary rays, per-lane walks for the rest unless
+// the variant knob says otherwise (32: reflection, 64: shadows of reflection hits, 128: shadows of
+// primary hits use packets when set... see kernel_variant)
+template <bool STATS>
+static void launch_full_pipeline(const FrameParams& P, int grid, hipStream_t st, int trav, int variant, bool hits,
+                                 hipEvent_t ev_m) {
+  const int q0 = 4 * grid;                    // primary waves (wcount0 entries)
+  const int lgrid = (P.W * P.H + 255) / 256;  // list kernels: worst case, every pixel listed
+  const int q1 = 4 * lgrid;                   // list waves (wcount1 entries)
+  const int t_refl = (variant & 32) ? TRAV_LANE : trav;
+  const int t_sh1 = (variant & 64) ? TRAV_LANE : trav;
+  const int t_sh0 = (variant & 128) ? TRAV_LANE : trav;
+  launch_trace<STATS>(P, grid, st, trav);  // + wcount0
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, st, (const uint32_t*)P.wcount0, P.woff0, q0, P.counters + 0);
+  hipLaunchKernelGGL(k_full_gen0, dim3(grid), dim3(256), 0, st, P);  // state0, refl, list0
+  launch_shadow<STATS>(P, lgrid, st, t_sh0, 0);
+  launch_refl<STATS>(P, lgrid, st, t_refl);
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, st, (const uint32_t*)P.wcount1, P.woff1, q1, P.counters + 1);
+  hipLaunchKernelGGL(k_full_gen1, dim3(lgrid), dim3(256), 0, st, P);  // state1, list1
+  launch_shadow<STATS>(P, lgrid, st, t_sh1, 1);
+  (void)hipEventRecord(ev_m, st);
+  if (hits) hipLaunchKernelGGL(k_full_final<true>, dim3(grid), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL(k_full_final<false>, dim3(grid), dim3(256), 0, st, P);
+}
+
+static int g_variant = -1;  // RT_KERNEL_VARIANT, or rt_debug_set_variant()
 static int kernel_variant() {
-  static int v = -1;
-  if (v < 0) {
+  if (g_variant < 0) {
     const char* e = getenv("RT_KERNEL_VARIANT");
-    v = e ? atoi(e) : 0;
+    g_variant = e ? atoi(e) : 0;
   }
-  return v;
+  return g_variant;
 }
 
 }  // namespace rt
@@ -918,6 +1376,12 @@ static int check_device_scene(rt_scene* s) {
   if (s->device == RT_DEVICE_NONE) { set_error("scene was created host-only (RT_DEVICE_NONE)"); return RT_ERR_NO_DEVICE; }
   HIPCHECK(hipSetDevice(s->device));
   return RT_OK;
+}
+
+extern "C" int rt_debug_set_variant(int32_t v) {
+  const int prev = kernel_variant();
+  g_variant = v < 0 ? 0 : v;
+  return prev;
 }
 
 extern "C" int rt_device_count(void) {
@@ -985,6 +1449,12 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   if (stats) HIPCHECK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st));
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
+  if (fr->mode == RT_MODE_FULL && (variant & 16)) {
+    // sized by the 16x16-padded frame: every wave of the tile grid has a count slot
+    const size_t npad = (size_t)P.tiles_x * 16 * (size_t)P.tiles_y * 16;
+    if ((rc = ensure_full(s, npad))) return rc;
+    bind_full(s, P);
+  }
   P.xcd_remap = (variant & 4) ? 1 : 0;
   const int trav = pick_trav(P, variant);
   if (s->ev_used + 3 > s->ev_pool.size()) {
@@ -1007,10 +1477,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       HIPCHECK(hipEventRecord(ev_m, st));
       if (hits) hipLaunchKernelGGL(k_shade_primary<true>, dim3(grid), dim3(256), 0, st, P);
       else hipLaunchKernelGGL(k_shade_primary<false>, dim3(grid), dim3(256), 0, st, P);
-    } else {
+    } else if (!(variant & 16)) {  // FULL as one kernel (default); 16 = the stage pipeline
       if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav); else launch_full<true, false>(P, grid, st, trav); }
       else { if (hits) launch_full<false, true>(P, grid, st, trav); else launch_full<false, false>(P, grid, st, trav); }
       HIPCHECK(hipEventRecord(ev_m, st));
+    } else {
+      if (stats) launch_full_pipeline<true>(P, grid, st, trav, variant, hits, ev_m);
+      else launch_full_pipeline<false>(P, grid, st, trav, variant, hits, ev_m);
     }
     HIPCHECK(hipGetLastError());
   } else {

@@ -97,6 +97,20 @@ struct DevScene {
   float Minv[16];          // getShapeModelMatrix().inverse() (object-space hit point for the box fast path)
 };
 
+// hit information handed between FULL stage kernels (32 B); face == 0xFFFFFFFF: no hit
+struct HitState {
+  float px, py, pz;
+  float nx, ny, nz;
+  int32_t mat;
+  uint32_t face;
+};
+// a ray handed between stages (32 B)
+struct RayRec {
+  float ox, oy, oz;
+  float dx, dy, dz;
+  uint32_t pad0, pad1;
+};
+
 // Per-launch parameters (kernel argument, ~1 KB)
 struct FrameParams {
   DevScene sc;
@@ -123,6 +137,21 @@ struct FrameParams {
   float* t_out;
   unsigned long long* stats;  // [8] counters (RT_FRAME_STATS)
   uint2* hits;                // [H][W] (t bits, triangle slot): PRIMARY trace -> shade hand-off
+  // FULL as a wavefront pipeline (per-pixel hand-off records between the stage kernels)
+  HitState* state0;           // [H][W] primary hit point / normal / material
+  HitState* state1;           // [H][W] reflection hit
+  RayRec* refl;               // [H][W] reflection ray (origin, direction)
+  uint2* hits1;               // [H][W] reflection closest hit (t bits, slot)
+  uint32_t* blk0;             // [H][W] per-light shadow bits of the primary hit
+  uint32_t* blk1;             // [H][W] per-light shadow bits of the reflection hit
+  uint32_t* list0;            // pixels whose primary ray hit, compacted in wave order (tile-coherent)
+  uint32_t* list1;            // pixels whose reflection ray hit, compacted in list0 order
+  uint32_t* wcount0;          // per primary wave: number of hit lanes (written by k_trace_primary)
+  uint32_t* wcount1;          // per list0 wave: number of reflection hits (written by k_full_refl)
+  uint32_t* woff0;            // exclusive prefix sums of wcount0 / wcount1 (k_scan_counts)
+  uint32_t* woff1;
+  uint32_t* counters;         // [0] = |list0|, [1] = |list1|
+  int32_t n_waves_max;        // list waves of the worst case (every pixel listed)
 };
 
 // Ray-list query parameters (rt_trace_closest / rt_trace_shadow)

@@ -76,6 +76,9 @@ struct rt_scene {
   int32_t* d_face = nullptr;
   float* d_t = nullptr;
   uint2* d_hits = nullptr;
+  // FULL wavefront pipeline buffers (allocated on the first FULL frame)
+  void* d_full = nullptr;
+  size_t full_pixels = 0;
   size_t fb_pixels = 0;
   int32_t last_W = 0, last_H = 0, last_flags = 0;
   int64_t last_rays = 0, last_total_rays = 0;

@@ -25,6 +25,7 @@ EXPORTS = [
     "rt_scene_ref_boxes", "rt_camera_flycam", "rt_render", "rt_render_async", "rt_synchronize",
     "rt_frame_download", "rt_trace_closest", "rt_trace_shadow", "rt_device_count", "rt_version",
     "rt_last_error", "rt_debug_math_host", "rt_debug_math_device", "rt_debug_validate_bvh",
+    "rt_debug_set_variant",
 ]
 
 
@@ -111,6 +112,7 @@ def lib():
         L.rt_debug_math_host.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_math_device.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
+        L.rt_debug_set_variant.argtypes = [C.c_int32]
         _lib = L
     return _lib
 
@@ -310,6 +312,11 @@ def write_ppm(path, rgb):
     rgb = np.ascontiguousarray(rgb, np.float32)
     H, W = rgb.shape[:2]
     check(lib().rt_write_ppm(os.fsencode(path), _p(rgb), W, H))
+
+
+def set_variant(v):
+    """Kernel-variant override (A/B and tests); returns the previous value."""
+    return lib().rt_debug_set_variant(int(v))
 
 
 def debug_math(op, inp, n, out_len, device=False):

@@ -186,3 +186,29 @@ def test_stats_counting_run(rt, soup):
     assert st["primary_rays"] == W * H
     assert st["node_visits"] > W * H and st["tri_tests"] > W * H
     assert st["wave_node_fetches"] * 16 < st["node_visits"]  # coherence: one fetch serves many rays
+
+
+VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "full-pipeline": 16, "pipeline-lane-refl": 48,
+            "pipeline-lane-all": 16 | 32 | 64 | 128}
+
+
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+def test_kernel_variants_render_identical_bits(rt, soup, name):
+    """Every A/B kernel variant (traversal flavour, FULL megakernel vs stage pipeline, per-lane walks)
+    renders exactly the default kernels' frame (rgb, face, t) on bunny (PRIMARY + FULL) and the 1M soup
+    (FULL, 640x360 crop of the C3 camera)."""
+    sc_soup, _ = soup
+    bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    cases = [(bunny, 1920, 1080, rt.RT_MODE_PRIMARY), (bunny, 1920, 1080, rt.RT_MODE_FULL),
+             (sc_soup, 640, 360, rt.RT_MODE_FULL)]
+    for sc, W, H, m in cases:
+        cam = rt.flycam(W, H, 0, 0, 20)
+        prev = rt.set_variant(0)
+        try:
+            ref = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+            rt.set_variant(VARIANTS[name])
+            got = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        finally:
+            rt.set_variant(prev)
+        for a, b in zip(ref[:3], got[:3]):
+            assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (name, W, H, m)
