@@ -92,6 +92,10 @@ def shard_tiles(W, H, rank, n):
     return [(t % tx, t // tx) for t in range(rank, tx * ((H + 15) // 16), n)]
 
 
+def backend_is_nccl(dist):
+    return dist is not None and dist.get_backend() == "nccl"
+
+
 def make_reducer(dist, dev):
     import torch
 
@@ -135,11 +139,17 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
+    ap.add_argument("--frames-in-flight", type=int, default=0,
+                    help="frames that may overlap on the GPU (0 = library default, 3)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob: BENCH_DEVICE pins every rank to one device (several ranks sharing one GPU, with
+    # BENCH_BACKEND=gloo for the timing reductions); unset in real runs (one GPU per rank)
+    if "BENCH_DEVICE" in os.environ:
+        local = int(os.environ["BENCH_DEVICE"])
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE {world} != --gpus {a.gpus}", file=sys.stderr)
     n = max(world, 1)
@@ -148,13 +158,13 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        backend = os.environ.get("BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device("cuda", local) if (torch.cuda.is_available() and backend_is_nccl(dist)) else torch.device("cpu")
 
     def barrier():
         if dist is not None:
@@ -171,8 +181,9 @@ def main():
     else:
         mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         scene_name = "Stanford bunny (69,451 triangles)"
-    sc = rt.Scene(mesh, device=local, leaf_size=a.leaf)
+    sc = rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight)
     info = sc.info()
+    info_fif = a.frames_in_flight or 3
     setup_s = time.perf_counter() - t0
     cam = rt.flycam(W, H, 0, 0, 20)
     mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY
@@ -261,6 +272,9 @@ def main():
             "config": {"workload": f"{cname}: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light",
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
                        "parallelism": f"tiles/{n} (16x16 tiles interleaved over ranks, scene replicated)",
+                       "frames_in_flight": info_fif,
+                       # per-frame latency (first kernel start to last kernel end of one frame); with
+                       # frames in flight, frames overlap and ms_per_step is the throughput interval
                        "kernel_ms_per_frame": round(kernel_ms_max, 4),
                        "trace_kernel_ms": round(trace_ms_max, 4),
                        "kernel_mrays_per_s": round(total_rays / a.steps / (kernel_ms_max * 1e-3) / 1e6, 2),

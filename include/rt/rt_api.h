@@ -96,6 +96,9 @@ typedef struct rt_scene_opts {
   int32_t leaf_size;      /* BVH leaf size bound (1..16), 0 = default */
   rt_material default_material; /* Flyscene::ka/kd/ks/shininess defaults (flyscene.hpp:179-184) */
   float background[3];    /* Flyscene::BACKGROUND_COLOR (flyscene.hpp:175) */
+  int32_t frames_in_flight; /* rt_render_async frames that may execute concurrently (1..4, default 3):
+                             * each in-flight frame has its own stream and frame buffers; frames stay
+                             * independent and rt_frame_download returns the most recent one */
 } rt_scene_opts;
 
 void rt_scene_opts_default(rt_scene_opts* o);

@@ -644,14 +644,30 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
 // ------------------------------------------------------------------------------------------------
 struct PixelCoord {
   int px, py, wv, lane;
+  int slot;   // this wave's LDS slot within its block
+  int qw;     // global wave number (tile-block * 4 + wave): the same for every block shape
   bool active;
 };
 
+// WPB = waves per block: 4 (one 256-thread block per 16x16 tile) or 1 (one 64-thread block per 8x8
+// quarter, blocks 4t..4t+3 cover tile t; finer-grained dispatch, same pixels and shard assignment)
+template <int WPB = 4>
 __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   PixelCoord c;
   c.lane = threadIdx.x & 63;
-  c.wv = (int)uniform(threadIdx.x >> 6);
-  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  int nb, b;
+  if (WPB == 4) {
+    c.wv = (int)uniform(threadIdx.x >> 6);
+    c.slot = c.wv;
+    nb = (int)gridDim.x;
+    b = (int)blockIdx.x;
+  } else {
+    c.wv = (int)(blockIdx.x & 3);
+    c.slot = 0;
+    nb = (int)(gridDim.x >> 2);
+    b = (int)(blockIdx.x >> 2);
+  }
+  c.qw = b * 4 + c.wv;
   int L = b;
   if (P.xcd_remap == 1) {
     const int q = nb >> 3, rr = nb & 7, x = b & 7, k = b >> 3;
@@ -695,22 +711,25 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
 #ifndef RT_TRACE_WAVES_PER_EU
 #define RT_TRACE_WAVES_PER_EU 8  // 8 waves/SIMD: measured +2.5% over the 7 the register count allows
 #endif
+#ifndef RT_TRACE_WPB
+#define RT_TRACE_WPB 1  // waves per block of the traversal kernel (4 or 1; 1 measured 3% faster)
+#endif
 template <bool STATS, int TRAV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
+__global__ __launch_bounds__(64 * RT_TRACE_WPB) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
 void k_trace_primary(FrameParams P) {
   __shared__ WaveLds<TRAV, STATS> lds;
-  const PixelCoord c = pixel_coord(P);
+  const PixelCoord c = pixel_coord<RT_TRACE_WPB>(P);
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && c.active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  trace<false, STATS, TRAV>(P.sc, r, c.active, h, dummy, lds, c.wv, cnt);
+  trace<false, STATS, TRAV>(P.sc, r, c.active, h, dummy, lds, c.slot, cnt);
   if (STATS && c.active && h.t != INFINITY) cnt[ST_HITS]++;
   if (c.active) P.hits[(size_t)c.py * P.W + c.px] = make_uint2(__float_as_uint(h.t), h.slot);
   if (P.wcount0 != nullptr) {  // FULL pipeline: per-wave hit count for the list0 compaction
     const uint32_t nh = (uint32_t)__popcll(ballot(c.active && h.t != INFINITY));
-    if (c.lane == 0) P.wcount0[blockIdx.x * 4 + c.wv] = nh;
+    if (c.lane == 0) P.wcount0[c.qw] = nh;
   }
   if (STATS) flush_stats(P, cnt, c.lane);
 }
@@ -929,7 +948,7 @@ __global__ __launch_bounds__(256) void k_full_gen0(FrameParams P) {
   const float t = c.active ? __uint_as_float(P.hits[pix].x) : INFINITY;
   // scatter this wave's hit pixels into list0 (offsets from the primary kernel's counts)
   const uint64_t hm = ballot(t != INFINITY);
-  if (t != INFINITY) P.list0[P.woff0[blockIdx.x * 4 + c.wv] + lanes_below(hm)] = (uint32_t)pix;
+  if (t != INFINITY) P.list0[P.woff0[c.qw] + lanes_below(hm)] = (uint32_t)pix;
   if (!c.active) return;
   const uint2 hb = P.hits[pix];
   HitState hs = no_hit_state();
@@ -1168,9 +1187,13 @@ int device_upload(rt_scene* s) {
   if (dev >= ndev) { set_error("device %d out of range (%d devices)", dev, ndev); return RT_ERR_INVALID; }
   HIPCHECK(hipSetDevice(dev));
   s->device = dev;
-  hipStream_t st;
-  HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  s->stream = st;
+  s->n_slots = std::max(1, std::min((int)s->opts.frames_in_flight, (int)rt_scene::kMaxSlots));
+  for (int k = 0; k < s->n_slots; k++) {
+    hipStream_t st;
+    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    s->slots[k].stream = st;
+  }
+  s->stream = s->slots[0].stream;
   HostScene& hs = s->hs;
   int64_t& tot = s->device_bytes;
   tot = 0;
@@ -1211,14 +1234,21 @@ int device_upload(rt_scene* s) {
 void device_release(rt_scene* s) {
   if (s->device == RT_DEVICE_NONE) return;
   (void)hipSetDevice(s->device);
-  if (s->stream) (void)hipStreamSynchronize((hipStream_t)s->stream);
-  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats,
-                  s->d_rgb, s->d_face, s->d_t, s->d_hits, s->d_full};
+  for (int k = 0; k < s->n_slots; k++)
+    if (s->slots[k].stream) (void)hipStreamSynchronize((hipStream_t)s->slots[k].stream);
+  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  for (int k = 0; k < s->n_slots; k++) {
+    rt_scene::FrameSlot& f = s->slots[k];
+    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_full};
+    for (void* b : fb)
+      if (b) (void)hipFree(b);
+    if (f.stream) (void)hipStreamDestroy((hipStream_t)f.stream);
+    f = rt_scene::FrameSlot{};
+  }
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
   s->ev_pool.clear();
-  if (s->stream) (void)hipStreamDestroy((hipStream_t)s->stream);
   s->stream = nullptr;
 }
 
@@ -1249,18 +1279,19 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
 // list1 (4 B) per pixel; then per list wave wcount0/1, woff0/1; then the counters
 constexpr size_t kFullBytesPerPixel = 32 + 32 + 32 + 8 + 4 + 4 + 4 + 4;
 static size_t full_waves(size_t npix) { return (npix + 63) / 64 + 8; }
-static int ensure_full(rt_scene* s, size_t npix) {
-  if (npix <= s->full_pixels) return RT_OK;
-  if (s->d_full) (void)hipFree(s->d_full);
-  s->d_full = nullptr;
-  s->full_pixels = 0;
-  HIPCHECK(hipMalloc(&s->d_full, npix * kFullBytesPerPixel + 16 * full_waves(npix) + 64));
-  s->full_pixels = npix;
+static int ensure_full(rt_scene::FrameSlot& f, size_t npix) {
+  if (npix <= f.full_pixels) return RT_OK;
+  HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));  // the slot's previous frames may still read it
+  if (f.d_full) (void)hipFree(f.d_full);
+  f.d_full = nullptr;
+  f.full_pixels = 0;
+  HIPCHECK(hipMalloc(&f.d_full, npix * kFullBytesPerPixel + 16 * full_waves(npix) + 64));
+  f.full_pixels = npix;
   return RT_OK;
 }
-static void bind_full(const rt_scene* s, FrameParams& P) {
-  char* b = (char*)s->d_full;
-  const size_t n = s->full_pixels;
+static void bind_full(const rt_scene::FrameSlot& f, FrameParams& P) {
+  char* b = (char*)f.d_full;
+  const size_t n = f.full_pixels;
   P.state0 = (HitState*)b;
   P.state1 = (HitState*)(b + 32 * n);
   P.refl = (RayRec*)(b + 64 * n);
@@ -1279,18 +1310,20 @@ static void bind_full(const rt_scene* s, FrameParams& P) {
   P.n_waves_max = (int32_t)q;
 }
 
-static int ensure_fb(rt_scene* s, size_t npix) {
-  if (npix <= s->fb_pixels) return RT_OK;
-  if (s->d_rgb) (void)hipFree(s->d_rgb);
-  if (s->d_face) (void)hipFree(s->d_face);
-  if (s->d_t) (void)hipFree(s->d_t);
-  if (s->d_hits) (void)hipFree(s->d_hits);
-  s->d_rgb = nullptr; s->d_face = nullptr; s->d_t = nullptr; s->d_hits = nullptr;
-  HIPCHECK(hipMalloc((void**)&s->d_rgb, npix * 12));
-  HIPCHECK(hipMalloc((void**)&s->d_face, npix * 4));
-  HIPCHECK(hipMalloc((void**)&s->d_t, npix * 4));
-  HIPCHECK(hipMalloc((void**)&s->d_hits, npix * 8));
-  s->fb_pixels = npix;
+static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
+  if (npix <= f.fb_pixels) return RT_OK;
+  HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));  // the slot's previous frames may still use them
+  if (f.d_rgb) (void)hipFree(f.d_rgb);
+  if (f.d_face) (void)hipFree(f.d_face);
+  if (f.d_t) (void)hipFree(f.d_t);
+  if (f.d_hits) (void)hipFree(f.d_hits);
+  f.d_rgb = nullptr; f.d_face = nullptr; f.d_t = nullptr; f.d_hits = nullptr;
+  f.fb_pixels = 0;
+  HIPCHECK(hipMalloc((void**)&f.d_rgb, npix * 12));
+  HIPCHECK(hipMalloc((void**)&f.d_face, npix * 4));
+  HIPCHECK(hipMalloc((void**)&f.d_t, npix * 4));
+  HIPCHECK(hipMalloc((void**)&f.d_hits, npix * 8));
+  f.fb_pixels = npix;
   return RT_OK;
 }
 
@@ -1307,9 +1340,10 @@ static int pick_trav(const FrameParams& P, int variant) {
 }
 template <bool STATS>
 static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int trav) {
-  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_B2_VGPR>), dim3(grid), dim3(256), 0, st, P);
-  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P);
-  else hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_W4>), dim3(grid), dim3(256), 0, st, P);
+  const dim3 g(grid * (4 / RT_TRACE_WPB)), b(64 * RT_TRACE_WPB);
+  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_B2_VGPR>), g, b, 0, st, P);
+  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_B2_LDS>), g, b, 0, st, P);
+  else hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_W4>), g, b, 0, st, P);
 }
 template <bool STATS, bool HITS>
 static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav) {
@@ -1404,7 +1438,11 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const int si = fr->shard_index;
   if (si < 0 || si >= sc) { set_error("rt_render: shard %d of %d", si, sc); return RT_ERR_INVALID; }
   const size_t npix = (size_t)fr->width * fr->height;
-  if ((rc = ensure_fb(s, npix))) return rc;
+  // frames in flight: round-robin over the slots; a slot's stream orders its own frames, frames on
+  // different slots overlap (tail of one frame with the start of the next)
+  const int slot_id = s->next_slot;
+  rt_scene::FrameSlot& slot = s->slots[slot_id];
+  if ((rc = ensure_fb(slot, npix))) return rc;
   FrameParams P;
   fill_scene_params(s, P);
   // camera (camera.hpp:115-118,155-173,263-266)
@@ -1438,22 +1476,27 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   P.n_tiles_shard = ntiles > si ? (ntiles - si + sc - 1) / sc : 0;
   P.mode = fr->mode;
   P.flags = fr->flags;
-  P.rgb = s->d_rgb;
-  P.face_out = s->d_face;
-  P.t_out = s->d_t;
+  P.rgb = slot.d_rgb;
+  P.face_out = slot.d_face;
+  P.t_out = slot.d_t;
   P.stats = s->d_stats;
-  P.hits = s->d_hits;
-  hipStream_t st = (hipStream_t)s->stream;
+  P.hits = slot.d_hits;
+  hipStream_t st = (hipStream_t)slot.stream;
   const bool stats = (fr->flags & RT_FRAME_STATS) != 0;
   const bool hits = (fr->flags & RT_FRAME_WRITE_HITS) != 0;
-  if (stats) HIPCHECK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st));
+  if (stats) {
+    // the counters are shared: a counting frame waits for every frame in flight on the other slots
+    for (int k = 0; k < s->n_slots; k++)
+      if (k != slot_id && s->slots[k].last_done) HIPCHECK(hipStreamWaitEvent(st, (hipEvent_t)s->slots[k].last_done, 0));
+    HIPCHECK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st));
+  }
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
   if (fr->mode == RT_MODE_FULL && (variant & 16)) {
     // sized by the 16x16-padded frame: every wave of the tile grid has a count slot
     const size_t npad = (size_t)P.tiles_x * 16 * (size_t)P.tiles_y * 16;
-    if ((rc = ensure_full(s, npad))) return rc;
-    bind_full(s, P);
+    if ((rc = ensure_full(slot, npad))) return rc;
+    bind_full(slot, P);
   }
   P.xcd_remap = (variant & 4) ? 1 : 0;
   const int trav = pick_trav(P, variant);
@@ -1490,6 +1533,9 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     HIPCHECK(hipEventRecord(ev_m, st));
   }
   HIPCHECK(hipEventRecord(ev_b, st));
+  slot.last_done = ev_b;
+  s->last_slot = slot_id;
+  s->next_slot = (slot_id + 1) % s->n_slots;
   s->last_W = fr->width;
   s->last_H = fr->height;
   s->last_flags = fr->flags;
@@ -1507,8 +1553,15 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
 extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
   int rc = check_device_scene(s);
   if (rc) return rc;
-  HIPCHECK(hipStreamSynchronize((hipStream_t)s->stream));
-  struct Reset { rt_scene* s; ~Reset() { s->ev_used = 0; s->pending = false; } } reset_{s};
+  for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
+  struct Reset {
+    rt_scene* s;
+    ~Reset() {
+      s->ev_used = 0;
+      s->pending = false;
+      for (int k = 0; k < s->n_slots; k++) s->slots[k].last_done = nullptr;
+    }
+  } reset_{s};
   if (out) {
     memset(out, 0, sizeof *out);
     double tot = 0.0, trav = 0.0;
@@ -1541,12 +1594,14 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
 extern "C" int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t) {
   int rc = check_device_scene(s);
   if (rc) return rc;
-  HIPCHECK(hipStreamSynchronize((hipStream_t)s->stream));
+  const rt_scene::FrameSlot& f = s->slots[s->last_slot];
+  HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));
   const size_t npix = (size_t)s->last_W * s->last_H;
-  if (rgb) HIPCHECK(hipMemcpy(rgb, s->d_rgb, npix * 12, hipMemcpyDeviceToHost));
+  if (!f.d_rgb || npix > f.fb_pixels) { set_error("rt_frame_download: no frame rendered"); return RT_ERR_INVALID; }
+  if (rgb) HIPCHECK(hipMemcpy(rgb, f.d_rgb, npix * 12, hipMemcpyDeviceToHost));
   if ((face || t) && !(s->last_flags & RT_FRAME_WRITE_HITS)) { set_error("last frame was rendered without RT_FRAME_WRITE_HITS"); return RT_ERR_INVALID; }
-  if (face) HIPCHECK(hipMemcpy(face, s->d_face, npix * 4, hipMemcpyDeviceToHost));
-  if (t) HIPCHECK(hipMemcpy(t, s->d_t, npix * 4, hipMemcpyDeviceToHost));
+  if (face) HIPCHECK(hipMemcpy(face, f.d_face, npix * 4, hipMemcpyDeviceToHost));
+  if (t) HIPCHECK(hipMemcpy(t, f.d_t, npix * 4, hipMemcpyDeviceToHost));
   return RT_OK;
 }
 

@@ -394,6 +394,7 @@ extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
   o->min_faces = 300;       // flyscene.hpp:168
   o->max_boxes = INT32_MAX; // flyscene.hpp:169
   o->leaf_size = 0;
+  o->frames_in_flight = 3;
   for (int k = 0; k < 3; k++) { o->default_material.ka[k] = 0.2f; o->background[k] = 0.9f; }
   o->default_material.kd[0] = 0.9f; o->default_material.kd[1] = 0.9f; o->default_material.kd[2] = 0.0f;
   o->default_material.shininess = 0.0f;
@@ -892,6 +893,7 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   auto s = new rt_scene();
   if (opts) s->opts = *opts; else rt_scene_opts_default(&s->opts);
   if (s->opts.min_faces <= 0) s->opts.min_faces = 300;
+  s->opts.frames_in_flight = std::max(1, std::min(s->opts.frames_in_flight, (int32_t)rt_scene::kMaxSlots));
   if (s->opts.max_boxes <= 0) s->opts.max_boxes = INT32_MAX;
   const int leaf = s->opts.leaf_size > 0 ? s->opts.leaf_size : 4;
   rt::HostScene& hs = s->hs;

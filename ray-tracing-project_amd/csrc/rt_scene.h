@@ -59,7 +59,7 @@ struct rt_scene {
   double build_ms = 0.0;
   int32_t device = RT_DEVICE_NONE;
   // device state (rt_device.hip)
-  void* stream = nullptr;
+  void* stream = nullptr;        // = slots[0].stream (ray-list queries, uploads)
   std::vector<void*> ev_pool;   // event pairs, one per render launch since the last synchronize
   size_t ev_used = 0;
   rt::Node64* d_nodes = nullptr;
@@ -71,15 +71,21 @@ struct rt_scene {
   rt::DevMat* d_mats = nullptr;
   unsigned long long* d_stats = nullptr;
   int64_t device_bytes = 0;
-  // frame buffers (grown on demand)
-  float* d_rgb = nullptr;
-  int32_t* d_face = nullptr;
-  float* d_t = nullptr;
-  uint2* d_hits = nullptr;
-  // FULL wavefront pipeline buffers (allocated on the first FULL frame)
-  void* d_full = nullptr;
-  size_t full_pixels = 0;
-  size_t fb_pixels = 0;
+  // frames in flight: each slot has its own stream and frame buffers (grown on demand)
+  struct FrameSlot {
+    void* stream = nullptr;
+    float* d_rgb = nullptr;
+    int32_t* d_face = nullptr;
+    float* d_t = nullptr;
+    uint2* d_hits = nullptr;
+    size_t fb_pixels = 0;
+    void* d_full = nullptr;  // FULL stage-pipeline hand-off buffers
+    size_t full_pixels = 0;
+    void* last_done = nullptr;  // event after this slot's latest frame (since the last synchronize)
+  };
+  static constexpr int kMaxSlots = 4;
+  FrameSlot slots[kMaxSlots];
+  int n_slots = 1, next_slot = 0, last_slot = 0;
   int32_t last_W = 0, last_H = 0, last_flags = 0;
   int64_t last_rays = 0, last_total_rays = 0;
   bool pending = false;

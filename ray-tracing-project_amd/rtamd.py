@@ -43,7 +43,8 @@ class MeshDesc(C.Structure):
 
 class SceneOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("min_faces", C.c_int32), ("max_boxes", C.c_int32),
-                ("leaf_size", C.c_int32), ("default_material", Material), ("background", C.c_float * 3)]
+                ("leaf_size", C.c_int32), ("default_material", Material), ("background", C.c_float * 3),
+                ("frames_in_flight", C.c_int32)]
 
 
 class SceneInfo(C.Structure):
@@ -201,21 +202,23 @@ class Mesh:
             self.h = None
 
 
-def scene_opts(device=-1, min_faces=300, leaf_size=0):
+def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0):
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
     o.device = device
     o.min_faces = min_faces
     o.leaf_size = leaf_size
+    if frames_in_flight:
+        o.frames_in_flight = frames_in_flight
     return o
 
 
 class Scene:
-    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0):
+    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0):
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
         self.h = C.c_void_p()
         d = mesh.desc()
-        o = scene_opts(device, min_faces, leaf_size)
+        o = scene_opts(device, min_faces, leaf_size, frames_in_flight)
         check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
 
     def info(self):
