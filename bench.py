@@ -238,6 +238,9 @@ def main():
                 "bytes_per_ray_path": round(b_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
                 "hit": round(hit, 4),
                 "path_achieved_GBps": round(b_ray * st["primary_rays"] / (kernel_ms_avg * 1e-3) / 1e9, 1),
+                # the same bytes over the wall-clock interval per frame (frames overlap in flight)
+                "achieved_throughput_GBps": round((b_trace if mode == rt.RT_MODE_PRIMARY else b_ray) * st["primary_rays"]
+                                                  / (elapsed / a.steps) / 1e9, 1),
                 "wave_fetch_bytes_per_ray": round((64 * stats["wave_node_fetches"] + 64 * stats["wave_tri_fetches"]) / rays, 2)}
 
     cpu = None
