@@ -119,6 +119,16 @@ typedef struct rt_scene_info {
 } rt_scene_info;
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);
+
+/* Binary scene cache: rt_scene_save writes everything rt_scene_create derived from
+ * the mesh (world vertices, unit normals, the reference box partition and its face order, the BVHs and
+ * triangle records; versioned, with a content hash); rt_scene_load restores it and uploads it without
+ * OBJ parsing or any build. The build parameters (min_faces, max_boxes, leaf_size) come from the file;
+ * device, frames_in_flight, default_material and background from opts (NULL = defaults). A truncated,
+ * corrupt or foreign file fails with RT_ERR_IO. Renders of a loaded scene equal the original's bit for
+ * bit. */
+int rt_scene_save(const rt_scene* s, const char* path);
+int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_scene** out);
 /* reference boxes: bounds6 [n][6] (low xyz, high xyz, object space), counts [n], face_order [n_faces]
  * (faces in reference iteration order: box creation order, then in-box order). NULL = skip. */
 int rt_scene_ref_boxes(const rt_scene* s, float* bounds6, int32_t* counts, int32_t* face_order);

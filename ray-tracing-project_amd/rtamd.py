@@ -25,7 +25,7 @@ EXPORTS = [
     "rt_scene_ref_boxes", "rt_camera_flycam", "rt_render", "rt_render_async", "rt_synchronize",
     "rt_frame_download", "rt_trace_closest", "rt_trace_shadow", "rt_device_count", "rt_version",
     "rt_last_error", "rt_debug_math_host", "rt_debug_math_device", "rt_debug_validate_bvh",
-    "rt_debug_set_variant",
+    "rt_debug_set_variant", "rt_scene_save", "rt_scene_load",
 ]
 
 
@@ -114,6 +114,8 @@ def lib():
         L.rt_debug_math_device.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
+        L.rt_scene_save.argtypes = [vp, C.c_char_p]
+        L.rt_scene_load.argtypes = [C.c_char_p, C.POINTER(SceneOpts), C.POINTER(vp)]
         _lib = L
     return _lib
 
@@ -225,6 +227,20 @@ class Scene:
         i = SceneInfo()
         check(lib().rt_scene_get_info(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in i._fields_}
+
+    def save(self, path):
+        """Binary scene cache (rt_scene_save)."""
+        check(lib().rt_scene_save(self.h, os.fsencode(path)))
+
+    @classmethod
+    def load(cls, path, device=-1, frames_in_flight=0):
+        """Scene from a binary cache (rt_scene_load): no OBJ parsing, no builds."""
+        self = cls.__new__(cls)
+        self.mesh = None
+        self.h = C.c_void_p()
+        o = scene_opts(device, 300, 0, frames_in_flight)
+        check(lib().rt_scene_load(os.fsencode(path), C.byref(o), C.byref(self.h)))
+        return self
 
     def validate_bvh(self):
         """Host check of both trees (containment + exact leaf cover); returns the info counters."""

@@ -236,3 +236,18 @@ def test_frames_in_flight_are_independent(rt, soup):
         out = np.zeros((c[1], c[0], 3), np.float32)
         rt.lib().rt_frame_download(sc.h, out.ctypes.data, None, None)
         assert out.tobytes() == ref[c].tobytes(), fif
+
+
+def test_scene_cache_renders_identical_bits(rt, tmp_path):
+    """A scene restored from the binary cache renders the original's frame bit for bit (PRIMARY + FULL)."""
+    orig = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    p = tmp_path / "bunny.rtscene"
+    orig.save(p)
+    ld = rt.Scene.load(p)
+    W, H = 960, 540
+    cam = rt.flycam(W, H, 0, 0, 20)
+    for m in (rt.RT_MODE_PRIMARY, rt.RT_MODE_FULL):
+        a = orig.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        b = ld.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes()

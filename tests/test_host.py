@@ -164,3 +164,27 @@ def test_invalid_inputs_rejected(rt, tmp_path):
     bad.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 9\n")
     with pytest.raises(rt.RTError, match="out of range"):
         rt.Mesh.load_obj(str(bad))
+
+
+@pytest.mark.parametrize("name", ["cube", "bunny"])
+def test_scene_cache_roundtrip(rt, tmp_path, name):
+    """f1 binary scene cache: save -> load restores the same boxes, face order and BVHs (re-saving the
+    loaded scene reproduces the file byte for byte); damaged files are rejected."""
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path(name + ".obj")), device=rt.RT_DEVICE_NONE)
+    p1, p2 = tmp_path / "a.rtscene", tmp_path / "b.rtscene"
+    sc.save(p1)
+    ld = rt.Scene.load(p1, device=rt.RT_DEVICE_NONE)
+    a, b = sc.info(), ld.info()
+    for k in ("n_faces", "n_vertices", "n_ref_boxes", "bvh_nodes", "bvh_leaves", "bvh_depth"):
+        assert a[k] == b[k], k
+    for x, y in zip(sc.ref_boxes(), ld.ref_boxes()):
+        np.testing.assert_array_equal(x, y)
+    assert ld.validate_bvh()["ok"]
+    ld.save(p2)
+    assert p1.read_bytes() == p2.read_bytes()
+    raw = p1.read_bytes()
+    bad = tmp_path / "bad.rtscene"
+    for damaged in (raw[: len(raw) // 2], raw[:100] + bytes([raw[100] ^ 1]) + raw[101:], b"NOTASCENE" + raw[9:]):
+        bad.write_bytes(damaged)
+        with pytest.raises(rt.RTError):
+            rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
