@@ -83,6 +83,9 @@ void rt_generate_soup(int32_t n_tris, uint64_t seed, float* v3_out);
 /* Tucano::ImageImporter::writePPMImage (tucano/utils/ppmIO.hpp:135-156): P3, row 0 first,
  * min(255, (int)(255*c)). rgb is [H][W][3]. */
 int rt_write_ppm(const char* path, const float* rgb, int32_t width, int32_t height);
+/* The same P3 text from 8-bit values (rt_frame_download_rgb8); byte-identical to rt_write_ppm whenever
+ * that download reported exact = 1. */
+int rt_write_ppm_rgb8(const char* path, const uint8_t* rgb8, int32_t width, int32_t height);
 
 /* ---------------------------------------------------------------------------------------------
  * Scene (device-resident acceleration structure)
@@ -197,6 +200,11 @@ int rt_synchronize(rt_scene* s, rt_stats* stats);
 /* copies the last frame from the device: rgb [H][W][3]; face [H][W] (-1 miss) and t [H][W] need
  * RT_FRAME_WRITE_HITS. NULL = skip. */
 int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t);
+/* Output path: the last frame converted on the device to writePPMImage's 8-bit
+ * values min(255, (int)(255*c)) and downloaded at 3 B/px. *exact (may be NULL) = 1 when every value
+ * was in 0..255, i.e. the bytes are exactly the PPM's numbers; 0 when some colour was NaN or negative
+ * (clamped to 0 here; rt_frame_download + rt_write_ppm reproduce the reference's text then). */
+int rt_frame_download_rgb8(rt_scene* s, uint8_t* rgb8, int32_t* exact);
 
 /* calculateMinimumFace (flyscene.cpp:373-396) for n rays on the device: face -1 = miss (t = +inf) */
 int rt_trace_closest(rt_scene* s, int32_t n, const float* origins3, const float* dirs3, int32_t* face,

@@ -1158,6 +1158,24 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
   }
 }
 
+// Output path: the float frame -> the PPM's 8-bit values on the device, so the host
+// reads 3 B/px instead of 12. Value = min(255, (int)(255*c)) as writePPMImage computes it
+// (tucano/utils/ppmIO.hpp:135-156; x86 cvttss2si: NaN / out of range -> INT_MIN); values outside
+// 0..255 (NaN or negative colours) are clamped and flagged, so the caller knows when the 8-bit frame is
+// not exactly the PPM's numbers.
+__global__ __launch_bounds__(256) void k_frame_rgb8(const float* rgb, uint8_t* out, uint32_t n, uint32_t* anomaly) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  bool bad = false;
+  if (i < n) {
+    const float x = 255.0f * rgb[i];
+    int v = (x >= -2147483648.0f && x < 2147483648.0f) ? (int)x : INT_MIN;
+    v = min(255, v);
+    bad = v < 0;
+    out[i] = (uint8_t)max(v, 0);
+  }
+  if (ballot(bad) && lane_id() == 0) atomicOr(anomaly, 1u);
+}
+
 __global__ void k_debug_math(int op, int n, int in_len, int out_len, const float* in, float* out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) debug_math_case(op, in + (size_t)k * in_len, out + (size_t)k * out_len);
@@ -1241,7 +1259,7 @@ void device_release(rt_scene* s) {
     if (b) (void)hipFree(b);
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
-    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_full};
+    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full};
     for (void* b : fb)
       if (b) (void)hipFree(b);
     if (f.stream) (void)hipStreamDestroy((hipStream_t)f.stream);
@@ -1602,6 +1620,35 @@ extern "C" int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* 
   if ((face || t) && !(s->last_flags & RT_FRAME_WRITE_HITS)) { set_error("last frame was rendered without RT_FRAME_WRITE_HITS"); return RT_ERR_INVALID; }
   if (face) HIPCHECK(hipMemcpy(face, f.d_face, npix * 4, hipMemcpyDeviceToHost));
   if (t) HIPCHECK(hipMemcpy(t, f.d_t, npix * 4, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+extern "C" int rt_frame_download_rgb8(rt_scene* s, uint8_t* rgb8, int32_t* exact) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  if (!rgb8) { set_error("rt_frame_download_rgb8: null output"); return RT_ERR_INVALID; }
+  rt_scene::FrameSlot& f = s->slots[s->last_slot];
+  const size_t npix = (size_t)s->last_W * s->last_H;
+  if (!f.d_rgb || npix == 0 || npix > f.fb_pixels) { set_error("rt_frame_download_rgb8: no frame rendered"); return RT_ERR_INVALID; }
+  hipStream_t st = (hipStream_t)f.stream;
+  if (npix > f.rgb8_pixels) {
+    HIPCHECK(hipStreamSynchronize(st));
+    if (f.d_rgb8) (void)hipFree(f.d_rgb8);
+    f.d_rgb8 = nullptr;
+    f.rgb8_pixels = 0;
+    HIPCHECK(hipMalloc((void**)&f.d_rgb8, npix * 3 + 64));
+    f.rgb8_pixels = npix;
+  }
+  uint32_t* flag = (uint32_t*)(f.d_rgb8 + ((npix * 3 + 15) / 16) * 16);
+  HIPCHECK(hipMemsetAsync(flag, 0, 4, st));
+  const uint32_t n = (uint32_t)(npix * 3);
+  hipLaunchKernelGGL(k_frame_rgb8, dim3((n + 255) / 256), dim3(256), 0, st, (const float*)f.d_rgb, f.d_rgb8, n, flag);
+  HIPCHECK(hipGetLastError());
+  uint32_t h_flag = 0;
+  HIPCHECK(hipMemcpyAsync(rgb8, f.d_rgb8, npix * 3, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(&h_flag, flag, 4, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  if (exact) *exact = h_flag ? 0 : 1;
   return RT_OK;
 }
 

@@ -373,6 +373,33 @@ extern "C" int rt_write_ppm(const char* path, const float* rgb, int32_t W, int32
   return RT_OK;
 }
 
+// writePPMImage's text for 8-bit values (same bytes as rt_write_ppm when every value is in 0..255),
+// without per-number formatting calls: a table of the 256 "%d " strings
+extern "C" int rt_write_ppm_rgb8(const char* path, const uint8_t* rgb8, int32_t W, int32_t H) {
+  if (!path || !rgb8 || W <= 0 || H <= 0) { rt::set_error("rt_write_ppm_rgb8: invalid arguments"); return RT_ERR_INVALID; }
+  static char tab[256][4];
+  static uint8_t len[256];
+  static bool init = false;
+  if (!init) {
+    for (int v = 0; v < 256; v++) len[v] = (uint8_t)snprintf(tab[v], 5, "%d ", v);
+    init = true;
+  }
+  std::string out;
+  out.reserve((size_t)W * H * 12 + 64);
+  out += "P3\n" + std::to_string(W) + " " + std::to_string(H) + "\n255\n";
+  for (int32_t j = 0; j < H; j++) {
+    const uint8_t* row = rgb8 + (size_t)j * W * 3;
+    for (int32_t i = 0; i < 3 * W; i++) out.append(tab[row[i]], len[row[i]]);
+    out += "\n";
+  }
+  FILE* f = fopen(path, "wb");
+  if (!f) { rt::set_error("cannot write %s", path); return RT_ERR_IO; }
+  const size_t wr = fwrite(out.data(), 1, out.size(), f);
+  fclose(f);
+  if (wr != out.size()) { rt::set_error("short write %s", path); return RT_ERR_IO; }
+  return RT_OK;
+}
+
 extern "C" void rt_camera_flycam(int32_t W, int32_t H, float dx, float dy, float dz, rt_camera* c) {
   // Flycamera::translate (flycamera.hpp:196-202), yaw = identity at rotation_Y_axis = 0
   const float I9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};

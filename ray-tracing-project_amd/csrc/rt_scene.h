@@ -79,6 +79,8 @@ struct rt_scene {
     float* d_t = nullptr;
     uint2* d_hits = nullptr;
     size_t fb_pixels = 0;
+    uint8_t* d_rgb8 = nullptr;  // 8-bit output frame (+ a 4-byte anomaly flag after it)
+    size_t rgb8_pixels = 0;
     void* d_full = nullptr;  // FULL stage-pipeline hand-off buffers
     size_t full_pixels = 0;
     void* last_done = nullptr;  // event after this slot's latest frame (since the last synchronize)

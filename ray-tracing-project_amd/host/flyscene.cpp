@@ -73,16 +73,27 @@ double Flyscene::raytraceScene(int width, int height) {
     ls[i] = rt_light{{lights[i].first.x, lights[i].first.y, lights[i].first.z},
                      {lights[i].second.x, lights[i].second.y, lights[i].second.z}};
   }
-  last_image.assign((size_t)width * height * 3, 0.0f);
   rt_frame fr{width, height, mode, 0, 1, 0};
   rt_stats st;
   printf("ray tracing ...\n");
   const auto t0 = std::chrono::steady_clock::now();
-  if (rt_render(scene_, &cam, ls.data(), (int32_t)ls.size(), &fr, last_image.data(), &st) != RT_OK) {
+  // render, then the 8-bit frame (3 B/px over PCIe); the float frame only when some value falls outside
+  // the PPM's 0..255 (NaN / negative colours), where writePPMImage's own numbers are reproduced from it
+  if (rt_render(scene_, &cam, ls.data(), (int32_t)ls.size(), &fr, nullptr, &st) != RT_OK) {
     fprintf(stderr, "%s\n", rt_last_error());
     return -1.0;
   }
-  if (rt_write_ppm(output.c_str(), last_image.data(), width, height) != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
+  std::vector<uint8_t> rgb8((size_t)width * height * 3);
+  int32_t exact = 0;
+  int rc = rt_frame_download_rgb8(scene_, rgb8.data(), &exact);
+  if (rc == RT_OK && exact) {
+    rc = rt_write_ppm_rgb8(output.c_str(), rgb8.data(), width, height);
+  } else if (rc == RT_OK) {
+    last_image.assign((size_t)width * height * 3, 0.0f);
+    rc = rt_frame_download(scene_, last_image.data(), nullptr, nullptr);
+    if (rc == RT_OK) rc = rt_write_ppm(output.c_str(), last_image.data(), width, height);
+  }
+  if (rc != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
   const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   printf(" ray tracing done! \n\nTime it took to render(in seconds): %.6f (kernel %.3f ms)\n", wall, st.kernel_ms);
   return st.kernel_ms;

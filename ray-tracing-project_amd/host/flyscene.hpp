@@ -59,7 +59,7 @@ class Flyscene {
   std::vector<std::pair<Vec3, Vec3>> lights;
   int mode = RT_MODE_FULL;               // the reference traceRay (max_depth 2, shadows)
   std::string output = "result.ppm";
-  std::vector<float> last_image;         // [H][W][3]
+  std::vector<float> last_image;         // [H][W][3] float frame (kept only when the 8-bit path was inexact)
 
  private:
   Flycamera flycamera;

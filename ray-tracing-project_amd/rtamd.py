@@ -26,6 +26,7 @@ EXPORTS = [
     "rt_frame_download", "rt_trace_closest", "rt_trace_shadow", "rt_device_count", "rt_version",
     "rt_last_error", "rt_debug_math_host", "rt_debug_math_device", "rt_debug_validate_bvh",
     "rt_debug_set_variant", "rt_scene_save", "rt_scene_load",
+    "rt_frame_download_rgb8", "rt_write_ppm_rgb8",
 ]
 
 
@@ -115,6 +116,8 @@ def lib():
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
+        L.rt_frame_download_rgb8.argtypes = [vp, vp, C.POINTER(C.c_int32)]
+        L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
         L.rt_scene_load.argtypes = [C.c_char_p, C.POINTER(SceneOpts), C.POINTER(vp)]
         _lib = L
     return _lib
@@ -204,9 +207,11 @@ class Mesh:
             self.h = None
 
 
-def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0):
+def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None):
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
+    if background is not None:
+        o.background[:] = [float(x) for x in background]
     o.device = device
     o.min_faces = min_faces
     o.leaf_size = leaf_size
@@ -216,17 +221,24 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0):
 
 
 class Scene:
-    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0):
+    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None):
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
         self.h = C.c_void_p()
         d = mesh.desc()
-        o = scene_opts(device, min_faces, leaf_size, frames_in_flight)
+        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background)
         check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
 
     def info(self):
         i = SceneInfo()
         check(lib().rt_scene_get_info(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in i._fields_}
+
+    def download_rgb8(self, W, H):
+        """The last frame as writePPMImage's 8-bit values (device conversion); returns (rgb8, exact)."""
+        out = np.zeros((H, W, 3), np.uint8)
+        ex = C.c_int32(0)
+        check(lib().rt_frame_download_rgb8(self.h, _p(out), C.byref(ex)))
+        return out, bool(ex.value)
 
     def save(self, path):
         """Binary scene cache (rt_scene_save)."""
@@ -336,6 +348,11 @@ def write_ppm(path, rgb):
 def set_variant(v):
     """Kernel-variant override (A/B and tests); returns the previous value."""
     return lib().rt_debug_set_variant(int(v))
+
+
+def write_ppm_rgb8(path, rgb8):
+    rgb8 = np.ascontiguousarray(rgb8, np.uint8)
+    check(lib().rt_write_ppm_rgb8(os.fsencode(path), _p(rgb8), rgb8.shape[1], rgb8.shape[0]))
 
 
 def debug_math(op, inp, n, out_len, device=False):

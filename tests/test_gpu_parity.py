@@ -251,3 +251,24 @@ def test_scene_cache_renders_identical_bits(rt, tmp_path):
         b = ld.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
         for x, y in zip(a[:3], b[:3]):
             assert np.asarray(x).tobytes() == np.asarray(y).tobytes()
+
+
+def test_rgb8_output_path(rt, tmp_path):
+    """f3: the device-side 8-bit conversion equals writePPMImage's numbers from the float frame, the PPM
+    written from it is byte-identical, and out-of-range colours are flagged (exact = False)."""
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    W, H = 1920, 1080
+    cam = rt.flycam(W, H, 0, 0, 20)
+    rgb, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_FULL)
+    v8, exact = sc.download_rgb8(W, H)
+    assert exact
+    ref = np.minimum(255, (np.float32(255) * rgb).astype(np.int64))
+    np.testing.assert_array_equal(v8, ref.astype(np.uint8))
+    a, b = tmp_path / "f.ppm", tmp_path / "b.ppm"
+    rt.write_ppm(a, rgb)
+    rt.write_ppm_rgb8(b, v8)
+    assert a.read_bytes() == b.read_bytes()
+    neg = rt.Scene(rt.Mesh.load_obj(scene_path("cube.obj")), background=(-0.5, 0.9, 2.0))
+    neg.render(rt.flycam(64, 48), rt.DEFAULT_LIGHTS, 64, 48)
+    v8, exact = neg.download_rgb8(64, 48)
+    assert not exact and v8[0, 0].tolist() == [0, 229, 255]

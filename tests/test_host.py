@@ -188,3 +188,15 @@ def test_scene_cache_roundtrip(rt, tmp_path, name):
         bad.write_bytes(damaged)
         with pytest.raises(rt.RTError):
             rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
+
+
+def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
+    """f3: the 8-bit P3 writer produces writePPMImage's exact bytes for in-range values."""
+    rng = np.random.default_rng(3)
+    rgb = rng.uniform(0, 1, (37, 53, 3)).astype(np.float32)
+    rgb[0, 0] = [0.0, 1.0, 0.999]
+    a, b = tmp_path / "a.ppm", tmp_path / "b.ppm"
+    rt.write_ppm(a, rgb)
+    v = np.minimum(255, (np.float32(255) * rgb).astype(np.int64)).astype(np.uint8)
+    rt.write_ppm_rgb8(b, v)
+    assert a.read_bytes() == b.read_bytes()
