@@ -92,6 +92,41 @@ def shard_tiles(W, H, rank, n):
     return [(t % tx, t // tx) for t in range(rank, tx * ((H + 15) // 16), n)]
 
 
+def e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist, iters=5):
+    """End-to-end frame with the output path: render this rank's tiles, pack them as 8-bit,
+    gather every rank's slice on rank 0 (RCCL all-gather over xGMI; gloo via host when rehearsing), unpack
+    there and copy the 8-bit frame to the host. Not the bench value: the PCIe-inclusive latency."""
+    import torch
+    slice_b = rt.shard_bytes(W, H, n)
+    on_gpu = dist is None or backend_is_nccl(dist)
+    slc = torch.empty(slice_b, dtype=torch.uint8, device="cuda")
+    gathered = torch.empty(n * slice_b, dtype=torch.uint8, device="cuda" if on_gpu else "cpu")
+    frame = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters + 1):
+        if dist is not None:
+            dist.barrier()
+        t = time.perf_counter()
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=(rank, n))
+        sc.synchronize()
+        if n == 1:
+            host, _ = sc.download_rgb8(W, H)
+        else:
+            sc.pack_shard_rgb8(slc.data_ptr())
+            if on_gpu:
+                dist.all_gather_into_tensor(gathered, slc)
+            else:
+                dist.all_gather_into_tensor(gathered, slc.cpu())
+            if rank == 0:
+                src = gathered if on_gpu else gathered.cuda()
+                torch.cuda.synchronize()
+                rt.unpack_shards_rgb8(src.data_ptr(), n, W, H, frame.data_ptr(), torch.cuda.current_device())
+                host = frame.cpu()
+        ts.append((time.perf_counter() - t) * 1e3)
+    return sorted(ts[1:])[len(ts[1:]) // 2]
+
+
 def backend_is_nccl(dist):
     return dist is not None and dist.get_backend() == "nccl"
 
@@ -138,6 +173,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + 8-bit frame to host) timing")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames that may overlap on the GPU (0 = library default, 3)")
@@ -243,6 +279,10 @@ def main():
                                                   / (elapsed / a.steps) / 1e9, 1),
                 "wave_fetch_bytes_per_ray": round((64 * stats["wave_node_fetches"] + 64 * stats["wave_tri_fetches"]) / rays, 2)}
 
+    e2e = None
+    if not a.no_e2e and torch.cuda.is_available():
+        e2e = reduce(e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist), "MAX")
+
     cpu = None
     if rank == 0 and n == 1 and not a.no_cpu:
         threads = min(16, os.cpu_count() or 1)
@@ -256,6 +296,9 @@ def main():
         else:
             cname = "C5" if a.mode == "full" else "C2"
         extra = {}
+        if e2e is not None:
+            # one frame end to end: render + 8-bit frame assembled on rank 0 (RCCL all-gather for N>1) + D2H
+            extra["e2e_frame_ms"] = round(e2e, 3)
         if stats is not None:
             extra["rays_per_frame_total"] = stats["total_rays"]  # primary + shadow + reflection (FULL)
             extra["total_mrays_per_s"] = round(stats["total_rays"] * n * a.steps / elapsed_max / 1e6, 2)

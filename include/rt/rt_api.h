@@ -206,6 +206,18 @@ int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t);
  * (clamped to 0 here; rt_frame_download + rt_write_ppm reproduce the reference's text then). */
 int rt_frame_download_rgb8(rt_scene* s, uint8_t* rgb8, int32_t* exact);
 
+/* Multi-GPU frame assembly (f3). Each rank's slice holds the 8-bit values of its own 16x16 tiles
+ * (rt_frame.shard_index/shard_count of its last frame) in shard tile order, rt_frame_shard_bytes() long
+ * (equal for all ranks, so one RCCL gather / all-gather of the slices brings the frame to one GPU);
+ * rt_frame_unpack_shards_rgb8 turns the concatenated slices into the H x W x 3 frame. Both pointers are
+ * device memory on the scene's / the given device (e.g. torch tensors' data_ptr()); both calls return
+ * after their device work is complete, and the caller orders any earlier writes to those buffers made on
+ * other streams (the library's streams do not synchronise with the legacy default stream). */
+int64_t rt_frame_shard_bytes(int32_t width, int32_t height, int32_t shard_count);
+int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device);
+int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t shard_count, int32_t width, int32_t height,
+                                void* frame_device, int32_t device);
+
 /* calculateMinimumFace (flyscene.cpp:373-396) for n rays on the device: face -1 = miss (t = +inf) */
 int rt_trace_closest(rt_scene* s, int32_t n, const float* origins3, const float* dirs3, int32_t* face,
                      float* t, float* P3);

@@ -1176,6 +1176,42 @@ __global__ __launch_bounds__(256) void k_frame_rgb8(const float* rgb, uint8_t* o
   if (ballot(bad) && lane_id() == 0) atomicOr(anomaly, 1u);
 }
 
+// Multi-GPU frame assembly (f3): a rank packs the 8-bit values of its own 16x16 tiles contiguously
+// (tile order of its shard, 768 B per tile, pixels outside the frame zero) so that one gather of equal
+// slices (RCCL over xGMI) brings every shard to one GPU, which unpacks them into the frame.
+__device__ __forceinline__ uint8_t ppm_u8(float c) {
+  const float x = 255.0f * c;
+  const int v = (x >= -2147483648.0f && x < 2147483648.0f) ? (int)x : INT_MIN;
+  return (uint8_t)max(min(255, v), 0);
+}
+__global__ __launch_bounds__(256) void k_pack_shard(const float* rgb, uint8_t* out, int W, int H, int tiles_x,
+                                                    int si, int sc, int n_tiles) {
+  const int L = blockIdx.x;  // one block per tile of the shard, one thread per pixel
+  if (L >= n_tiles) return;
+  const int tile = si + L * sc;
+  const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
+  uint8_t* o = out + ((size_t)L * 256 + threadIdx.x) * 3;
+  if (x < W && y < H) {
+    const float* c = rgb + 3 * ((size_t)y * W + x);
+    o[0] = ppm_u8(c[0]);
+    o[1] = ppm_u8(c[1]);
+    o[2] = ppm_u8(c[2]);
+  } else {
+    o[0] = o[1] = o[2] = 0;
+  }
+}
+__global__ __launch_bounds__(256) void k_unpack_shards(const uint8_t* packed, uint8_t* frame, int W, int H, int tiles_x,
+                                                       int n, size_t slice_bytes) {
+  const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (size_t)W * H) return;
+  const int x = (int)(p % W), y = (int)(p / W);
+  const int t = (y >> 4) * tiles_x + (x >> 4);
+  const uint8_t* src = packed + (size_t)(t % n) * slice_bytes + ((size_t)(t / n) * 256 + (y & 15) * 16 + (x & 15)) * 3;
+  frame[3 * p + 0] = src[0];
+  frame[3 * p + 1] = src[1];
+  frame[3 * p + 2] = src[2];
+}
+
 __global__ void k_debug_math(int op, int n, int in_len, int out_len, const float* in, float* out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) debug_math_case(op, in + (size_t)k * in_len, out + (size_t)k * out_len);
@@ -1556,6 +1592,8 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   s->next_slot = (slot_id + 1) % s->n_slots;
   s->last_W = fr->width;
   s->last_H = fr->height;
+  s->last_shard_index = si;
+  s->last_shard_count = sc;
   s->last_flags = fr->flags;
   // primary rays of this shard: pixels inside the frame of the shard's tiles
   int64_t rays = 0;
@@ -1649,6 +1687,49 @@ extern "C" int rt_frame_download_rgb8(rt_scene* s, uint8_t* rgb8, int32_t* exact
   HIPCHECK(hipMemcpyAsync(&h_flag, flag, 4, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
   if (exact) *exact = h_flag ? 0 : 1;
+  return RT_OK;
+}
+
+extern "C" int64_t rt_frame_shard_bytes(int32_t W, int32_t H, int32_t shard_count) {
+  if (W <= 0 || H <= 0 || shard_count <= 0) return 0;
+  const int64_t ntiles = (int64_t)((W + 15) / 16) * ((H + 15) / 16);
+  return (ntiles + shard_count - 1) / shard_count * 768;
+}
+
+extern "C" int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  if (!dst_device) { set_error("rt_frame_pack_shard_rgb8: null destination"); return RT_ERR_INVALID; }
+  rt_scene::FrameSlot& f = s->slots[s->last_slot];
+  if (!f.d_rgb || (size_t)s->last_W * s->last_H > f.fb_pixels) { set_error("rt_frame_pack_shard_rgb8: no frame rendered"); return RT_ERR_INVALID; }
+  const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, ntiles = tiles_x * ((H + 15) / 16);
+  const int si = s->last_shard_index, sc = s->last_shard_count;
+  const int n_tiles = ntiles > si ? (ntiles - si + sc - 1) / sc : 0;
+  hipStream_t st = (hipStream_t)f.stream;
+  const int64_t slice = rt_frame_shard_bytes(W, H, sc);
+  if ((int64_t)n_tiles * 768 < slice) HIPCHECK(hipMemsetAsync((uint8_t*)dst_device + (size_t)n_tiles * 768, 0, (size_t)(slice - (int64_t)n_tiles * 768), st));
+  if (n_tiles > 0)
+    hipLaunchKernelGGL(k_pack_shard, dim3(n_tiles), dim3(256), 0, st, (const float*)f.d_rgb, (uint8_t*)dst_device, W, H,
+                       tiles_x, si, sc, n_tiles);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));
+  return RT_OK;
+}
+
+extern "C" int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t shard_count, int32_t W, int32_t H,
+                                           void* frame_device, int32_t device) {
+  if (!packed_device || !frame_device || shard_count <= 0 || W <= 0 || H <= 0) {
+    set_error("rt_frame_unpack_shards_rgb8: invalid arguments");
+    return RT_ERR_INVALID;
+  }
+  int dev = device;
+  if (dev < 0) HIPCHECK(hipGetDevice(&dev));
+  HIPCHECK(hipSetDevice(dev));
+  const size_t npix = (size_t)W * H;
+  hipLaunchKernelGGL(k_unpack_shards, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, 0, (const uint8_t*)packed_device,
+                     (uint8_t*)frame_device, W, H, (W + 15) / 16, shard_count, (size_t)rt_frame_shard_bytes(W, H, shard_count));
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipDeviceSynchronize());
   return RT_OK;
 }
 

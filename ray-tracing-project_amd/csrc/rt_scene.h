@@ -88,7 +88,7 @@ struct rt_scene {
   static constexpr int kMaxSlots = 4;
   FrameSlot slots[kMaxSlots];
   int n_slots = 1, next_slot = 0, last_slot = 0;
-  int32_t last_W = 0, last_H = 0, last_flags = 0;
+  int32_t last_W = 0, last_H = 0, last_flags = 0, last_shard_index = 0, last_shard_count = 1;
   int64_t last_rays = 0, last_total_rays = 0;
   bool pending = false;
 };

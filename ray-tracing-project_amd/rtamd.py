@@ -26,7 +26,8 @@ EXPORTS = [
     "rt_frame_download", "rt_trace_closest", "rt_trace_shadow", "rt_device_count", "rt_version",
     "rt_last_error", "rt_debug_math_host", "rt_debug_math_device", "rt_debug_validate_bvh",
     "rt_debug_set_variant", "rt_scene_save", "rt_scene_load",
-    "rt_frame_download_rgb8", "rt_write_ppm_rgb8",
+    "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
+    "rt_frame_unpack_shards_rgb8",
 ]
 
 
@@ -118,6 +119,10 @@ def lib():
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
         L.rt_frame_download_rgb8.argtypes = [vp, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
+        L.rt_frame_shard_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+        L.rt_frame_shard_bytes.restype = C.c_int64
+        L.rt_frame_pack_shard_rgb8.argtypes = [vp, vp]
+        L.rt_frame_unpack_shards_rgb8.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32]
         L.rt_scene_load.argtypes = [C.c_char_p, C.POINTER(SceneOpts), C.POINTER(vp)]
         _lib = L
     return _lib
@@ -240,6 +245,10 @@ class Scene:
         check(lib().rt_frame_download_rgb8(self.h, _p(out), C.byref(ex)))
         return out, bool(ex.value)
 
+    def pack_shard_rgb8(self, dst_device_ptr):
+        """This rank's tiles of the last frame, 8-bit, into device memory (rt_frame_pack_shard_rgb8)."""
+        check(lib().rt_frame_pack_shard_rgb8(self.h, C.c_void_p(dst_device_ptr)))
+
     def save(self, path):
         """Binary scene cache (rt_scene_save)."""
         check(lib().rt_scene_save(self.h, os.fsencode(path)))
@@ -348,6 +357,14 @@ def write_ppm(path, rgb):
 def set_variant(v):
     """Kernel-variant override (A/B and tests); returns the previous value."""
     return lib().rt_debug_set_variant(int(v))
+
+
+def shard_bytes(W, H, n):
+    return int(lib().rt_frame_shard_bytes(W, H, n))
+
+
+def unpack_shards_rgb8(packed_ptr, n, W, H, frame_ptr, device=-1):
+    check(lib().rt_frame_unpack_shards_rgb8(C.c_void_p(packed_ptr), n, W, H, C.c_void_p(frame_ptr), device))
 
 
 def write_ppm_rgb8(path, rgb8):

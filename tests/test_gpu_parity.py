@@ -272,3 +272,26 @@ def test_rgb8_output_path(rt, tmp_path):
     neg.render(rt.flycam(64, 48), rt.DEFAULT_LIGHTS, 64, 48)
     v8, exact = neg.download_rgb8(64, 48)
     assert not exact and v8[0, 0].tolist() == [0, 229, 255]
+
+
+def test_shard_pack_gather_unpack(rt, soup):
+    """f3 multi-GPU assembly on one device: every shard's packed 8-bit tiles, concatenated as an RCCL
+    gather would, unpack to the single-device frame's 8-bit values."""
+    import torch
+    sc, _ = soup
+    W, H = 1000, 600  # ragged: partial tiles at the right and bottom edges
+    cam = rt.flycam(W, H, 0, 0, 20)
+    sc.render(cam, rt.DEFAULT_LIGHTS, W, H)
+    ref, exact = sc.download_rgb8(W, H)
+    assert exact
+    for n in (1, 2, 3, 8):
+        slice_b = rt.shard_bytes(W, H, n)
+        packed = torch.zeros(n * slice_b, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch's fill must land before the library's own streams write
+        for k in range(n):
+            sc.render(cam, rt.DEFAULT_LIGHTS, W, H, shard=(k, n))
+            sc.pack_shard_rgb8(packed.data_ptr() + k * slice_b)
+        frame = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        rt.unpack_shards_rgb8(packed.data_ptr(), n, W, H, frame.data_ptr(), torch.cuda.current_device())
+        np.testing.assert_array_equal(frame.cpu().numpy().reshape(H, W, 3), ref)
