@@ -151,11 +151,35 @@ typedef struct rt_camera {
 void rt_camera_flycam(int32_t width, int32_t height, float dx, float dy, float dz, rt_camera* out);
 
 typedef struct rt_light {
-  float position[3]; /* Flyscene::lights[i].first  (flyscene.hpp:132) */
-  float color[3];    /* Flyscene::lights[i].second */
+  float position[3]; /* point: Flyscene::lights[i].first (flyscene.hpp:132); directional: the vector the
+                        reference stores as get<0>(dirLights[i]) (flyscene.hpp:135) and uses as the light
+                        direction as is (calculateColor, flyscene.cpp:610-612) */
+  float color[3];    /* Flyscene::lights[i].second / get<1>(dirLights[i]) */
+  int32_t kind;      /* RT_LIGHT_POINT or RT_LIGHT_DIRECTIONAL */
 } rt_light;
 
-#define RT_MAX_LIGHTS 16
+#define RT_LIGHT_POINT 0
+#define RT_LIGHT_DIRECTIONAL 1
+/* calculateColor sums every point light (in order), then every directional light (in order); the
+ * library applies that order whatever the order of the array. */
+#define RT_MAX_LIGHTS 32
+
+/* Light helpers. The reference draws sphere jitter from the C library's rand()
+ * without seeding it (flyscene.cpp:529-538); rt_rand_state reproduces glibc's rand() (TYPE_3 additive
+ * feedback generator, RAND_MAX 2^31-1), so seed 1 gives the sequence of a fresh reference process. */
+typedef struct rt_rand_state {
+  uint32_t r[34];
+  uint32_t k;
+} rt_rand_state;
+void rt_rand_seed(rt_rand_state* st, uint32_t seed);
+int32_t rt_rand(rt_rand_state* st);
+/* Flyscene::sphericalLight + addLight('s') (flyscene.cpp:212-239, 529-538): n_points jittered point lights
+ * (offset (-r + rand()/(RAND_MAX/(2r))) per axis, x then y then z) each with colour/(n_points+1), then the
+ * centre light with colour/(n_points+1); writes n_points + 1 lights to out and returns that count. */
+int32_t rt_lights_spherical(const rt_light* centre, float radius, int32_t n_points, rt_rand_state* rng, rt_light* out);
+/* addLight('d') (flyscene.cpp:242-246): the "direction" the reference stores is screenToWorld(viewport
+ * centre), a point (a point used as a direction); kind = RT_LIGHT_DIRECTIONAL. */
+void rt_light_directional(const rt_camera* cam, const float color[3], rt_light* out);
 
 enum { RT_MODE_PRIMARY = 0, RT_MODE_FULL = 1 };
 

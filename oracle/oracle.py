@@ -27,7 +27,7 @@ class Camera(C.Structure):
 
 class RenderOpts(C.Structure):
     _fields_ = [("max_depth", C.c_int32), ("shadows", C.c_int32), ("background", C.c_float * 3),
-                ("def_mat", C.c_float * 12)]
+                ("def_mat", C.c_float * 12), ("dir_lights6", C.c_void_p), ("n_dir_lights", C.c_int32)]
 
 
 def lib():
@@ -169,10 +169,14 @@ class Scene:
         lib().orc_shadow(self.h, len(P), P, L, out)
         return out
 
-    def render(self, cam, lights, W, H, full=False, pixels=None, threads=1):
-        """lights: [(pos3, color3), ...]. Returns rgb [n,3], face [n], t [n] (n = W*H or len(pixels))."""
+    def render(self, cam, lights, W, H, full=False, pixels=None, threads=1, dir_lights=()):
+        """lights: [(pos3, color3), ...] point lights; dir_lights: [(vector3, color3), ...] directional lights
+        (Flyscene::dirLights). Returns rgb [n,3], face [n], t [n] (n = W*H or len(pixels))."""
         opts = RenderOpts()
         lib().orc_render_opts_default(C.byref(opts), 1 if full else 0)
+        D6 = np.ascontiguousarray(np.array([list(p) + list(c) for p, c in dir_lights], np.float32).reshape(-1))
+        opts.dir_lights6 = D6.ctypes.data if len(dir_lights) else None
+        opts.n_dir_lights = len(dir_lights)
         L6 = np.ascontiguousarray(np.array([list(p) + list(c) for p, c in lights], np.float32).reshape(-1))
         if pixels is None:
             n = W * H

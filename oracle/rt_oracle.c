@@ -891,6 +891,13 @@ static void calc_color(const tctx* c, mstate* st, int32_t f, const float* o, con
     calc_single(c, st, f, o, L, lp + 3, P, col);
     sum[0] += col[0]; sum[1] += col[1]; sum[2] += col[2];
   }
+  /* directional lights: the stored vector is the light direction as is (flyscene.cpp:610-612) */
+  for (int32_t l = 0; l < c->opt->n_dir_lights; l++) {
+    const float* dl = &c->opt->dir_lights6[6 * l];
+    float L[3] = {dl[0], dl[1], dl[2]}, col[3];
+    calc_single(c, st, f, o, L, dl + 3, P, col);
+    sum[0] += col[0]; sum[1] += col[1]; sum[2] += col[2];
+  }
   for (int k = 0; k < 3; k++) out[k] = s_max(s_min(sum[k], 1.f), 0.f);
 }
 

@@ -69,6 +69,8 @@ typedef struct orc_render_opts {
   int32_t shadows;     /* 1 = shadow() any-hit per light (FULL), 0 = disabled (PRIMARY) */
   float background[3]; /* BACKGROUND_COLOR */
   float def_mat[ORC_MAT_FLOATS]; /* Flyscene default ka/kd/ks/shininess/.. (flyscene.hpp:179-184) */
+  const float* dir_lights6;      /* Flyscene::dirLights: [n][direction3, colour3] (flyscene.hpp:135) */
+  int32_t n_dir_lights;          /* summed after the point lights (calculateColor, flyscene.cpp:610-612) */
 } orc_render_opts;
 
 void orc_render_opts_default(orc_render_opts* o, int32_t full);

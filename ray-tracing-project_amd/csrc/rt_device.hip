@@ -588,6 +588,13 @@ __device__ __forceinline__ TriRec64 vload_tri(const TriRec64* base, uint32_t i) 
 // std::pow(float,float) -> powf: evaluated in fp64 then rounded (matches a correctly rounded powf)
 __device__ __forceinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }
 
+// calculateColor's light direction (flyscene.cpp:607-611): point light -(P - pos).normalized(), or a
+// directional light's stored vector as is
+__device__ __forceinline__ f3 light_dir(f3 p, const Light& l) {
+  if (l.kind == RT_LIGHT_DIRECTIONAL) return f3{l.p[0], l.p[1], l.p[2]};
+  return neg(normalized(sub(p, f3{l.p[0], l.p[1], l.p[2]})));
+}
+
 // Hit information of one lane, gathered once and reused by every light of calculateColor
 struct HitInfo {
   f3 p, n;
@@ -616,8 +623,7 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
                                          WaveLds<TRAV, STATS>* lds, int wv, uint32_t* cnt) {
   f3 sum{0.0f, 0.0f, 0.0f};
   for (int l = 0; l < P.n_lights; l++) {
-    const float* lp = P.lights[l].p;
-    const f3 L = neg(normalized(sub(hi.p, f3{lp[0], lp[1], lp[2]})));
+    const f3 L = light_dir(hi.p, P.lights[l]);
     bool blocked = false;
     if (SHADOWS) {
       Ray sr;
@@ -984,8 +990,7 @@ void k_full_shadow(FrameParams P, int pass) {
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
   uint32_t bits = 0;
   for (int l = 0; l < P.n_lights; l++) {
-    const float* lp = P.lights[l].p;
-    const f3 Ld = neg(normalized(sub(p, f3{lp[0], lp[1], lp[2]})));
+    const f3 Ld = light_dir(p, P.lights[l]);
     Ray sr;
     sr.o = offset(p, Ld, 0.003f);
     sr.d = Ld;
@@ -1062,8 +1067,7 @@ __device__ __forceinline__ f3 calc_color_bits(const FrameParams& P, MatState& st
                                               uint32_t bits) {
   f3 sum{0.0f, 0.0f, 0.0f};
   for (int l = 0; l < P.n_lights; l++) {
-    const float* lp = P.lights[l].p;
-    const f3 L = neg(normalized(sub(hi.p, f3{lp[0], lp[1], lp[2]})));
+    const f3 L = light_dir(hi.p, P.lights[l]);
     const bool blocked = (bits >> l) & 1u;
     f3 c{0.0f, 0.0f, 0.0f};
     if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
@@ -1516,9 +1520,17 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   P.xscale = cam->aspect_ratio * scale;
   P.yscale = scale;
   P.n_lights = n_lights;
-  for (int l = 0; l < n_lights; l++) {
-    memcpy(P.lights[l].p, lights[l].position, 12);
-    memcpy(P.lights[l].c, lights[l].color, 12);
+  {  // calculateColor's order: point lights first, then directional lights (each in array order)
+    int k = 0;
+    for (int pass = 0; pass < 2; pass++)
+      for (int l = 0; l < n_lights; l++) {
+        const int kind = lights[l].kind == RT_LIGHT_DIRECTIONAL ? RT_LIGHT_DIRECTIONAL : RT_LIGHT_POINT;
+        if (kind != (pass ? RT_LIGHT_DIRECTIONAL : RT_LIGHT_POINT)) continue;
+        memcpy(P.lights[k].p, lights[l].position, 12);
+        memcpy(P.lights[k].c, lights[l].color, 12);
+        P.lights[k].kind = kind;
+        k++;
+      }
   }
   P.W = fr->width;
   P.H = fr->height;

@@ -400,6 +400,81 @@ extern "C" int rt_write_ppm_rgb8(const char* path, const uint8_t* rgb8, int32_t 
   return RT_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Lights
+// ---------------------------------------------------------------------------------------------------
+// glibc rand(): TYPE_3 additive feedback generator, r[i] = r[i-31] + r[i-3] (mod 2^32) after a
+// Park-Miller seeding of r[0..30], r[31..33] = r[0..2] and 310 discarded outputs; rand() = r[i] >> 1.
+// The state is the ring of the last 34 values.
+extern "C" void rt_rand_seed(rt_rand_state* st, uint32_t seed) {
+  if (!st) return;
+  uint32_t r[344];
+  r[0] = seed ? seed : 1u;
+  for (int i = 1; i < 31; i++) {
+    const int64_t w = (16807LL * (int64_t)(int32_t)r[i - 1]) % 2147483647LL;
+    r[i] = (uint32_t)(w < 0 ? w + 2147483647LL : w);
+  }
+  for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+  for (int i = 34; i < 344; i++) r[i] = r[i - 31] + r[i - 3];
+  for (int i = 310; i < 344; i++) st->r[i % 34] = r[i];
+  st->k = 344 % 34;
+}
+
+extern "C" int32_t rt_rand(rt_rand_state* st) {
+  const uint32_t k = st->k;  // slot of r[i - 34]; r[i - 31] is k + 3, r[i - 3] is k + 31 (mod 34)
+  const uint32_t v = st->r[(k + 3) % 34] + st->r[(k + 31) % 34];
+  st->r[k] = v;
+  st->k = (k + 1) % 34;
+  return (int32_t)(v >> 1);
+}
+
+extern "C" int32_t rt_lights_spherical(const rt_light* centre, float radius, int32_t n_points, rt_rand_state* rng,
+                                       rt_light* out) {
+  if (!centre || !out || n_points < 0) { rt::set_error("rt_lights_spherical: invalid arguments"); return RT_ERR_INVALID; }
+  rt_rand_state local;
+  if (!rng) { rt_rand_seed(&local, 1); rng = &local; }
+  const float div = (float)(n_points + 1);
+  float col[3];
+  for (int k = 0; k < 3; k++) col[k] = centre->color[k] / div;  // light.second / (nLightpoints + 1)
+  for (int32_t i = 0; i < n_points; i++) {
+    float off[3];
+    for (int k = 0; k < 3; k++) {  // -radius + (rand() / (RAND_MAX / (radius * 2))), x then y then z
+      const float q = (float)2147483647 / (radius * 2);
+      off[k] = -radius + ((float)rt_rand(rng) / q);
+    }
+    for (int k = 0; k < 3; k++) {
+      out[i].position[k] = centre->position[k] + off[k];
+      out[i].color[k] = col[k];
+    }
+    out[i].kind = RT_LIGHT_POINT;
+  }
+  for (int k = 0; k < 3; k++) {
+    out[n_points].position[k] = centre->position[k];
+    out[n_points].color[k] = col[k];  // light.second /= (Nlights + 1)
+  }
+  out[n_points].kind = RT_LIGHT_POINT;
+  return n_points + 1;
+}
+
+extern "C" void rt_light_directional(const rt_camera* c, const float color[3], rt_light* out) {
+  // screenToWorld(Vector2f(viewport(2) / 2, viewport(3) / 2)) (camera.hpp:155-173), the point itself
+  const float px = c->viewport[2] / 2, py = c->viewport[3] / 2;
+  f3 nc;
+  nc.x = (float)(2.0 * (double)(px - c->viewport[0]) / (double)c->viewport[2] - 1.0);
+  nc.y = (float)(1.0 - 2.0 * (double)(py - c->viewport[1]) / (double)c->viewport[3]);
+  nc.z = -1.0f;
+  const float persp = (float)((double)1.0f / tan((double)(c->fovy / 2.0f) * (M_PI / 180.0)));
+  const float scale = (float)(1.0 / (double)persp);
+  nc.x = nc.x * (c->aspect_ratio * scale);
+  nc.y = nc.y * scale;
+  float vinv[16];
+  rt::affinv(c->view_matrix, vinv);
+  const f3 w = rt::affv3(vinv, nc);
+  out->position[0] = w.x; out->position[1] = w.y; out->position[2] = w.z;
+  for (int k = 0; k < 3; k++) out->color[k] = color[k];
+  out->kind = RT_LIGHT_DIRECTIONAL;
+}
+
 extern "C" void rt_camera_flycam(int32_t W, int32_t H, float dx, float dy, float dz, rt_camera* c) {
   // Flycamera::translate (flycamera.hpp:196-202), yaw = identity at rotation_Y_axis = 0
   const float I9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};

@@ -79,6 +79,7 @@ struct alignas(16) DevMat {
 
 struct Light {
   float p[3], c[3];
+  int32_t kind;  // RT_LIGHT_POINT / RT_LIGHT_DIRECTIONAL
 };
 
 // Device scene view (pointers stay wave-uniform: SGPRs)
@@ -126,7 +127,7 @@ struct FrameParams {
   float xscale, yscale;    // aspect_ratio * scale, scale
   // lights
   int32_t n_lights;
-  Light lights[16];
+  Light lights[32];
   // frame
   int32_t W, H, tiles_x, tiles_y;  // tiles = 16x16 pixel blocks (one 256-thread block each)
   int32_t xcd_remap;

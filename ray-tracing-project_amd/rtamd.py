@@ -27,7 +27,7 @@ EXPORTS = [
     "rt_last_error", "rt_debug_math_host", "rt_debug_math_device", "rt_debug_validate_bvh",
     "rt_debug_set_variant", "rt_scene_save", "rt_scene_load",
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
-    "rt_frame_unpack_shards_rgb8",
+    "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
 ]
 
 
@@ -61,7 +61,14 @@ class Camera(C.Structure):
 
 
 class Light(C.Structure):
-    _fields_ = [("position", C.c_float * 3), ("color", C.c_float * 3)]
+    _fields_ = [("position", C.c_float * 3), ("color", C.c_float * 3), ("kind", C.c_int32)]
+
+
+RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL = 0, 1
+
+
+class RandState(C.Structure):
+    _fields_ = [("r", C.c_uint32 * 34), ("k", C.c_uint32)]
 
 
 class Frame(C.Structure):
@@ -120,6 +127,14 @@ def lib():
         L.rt_frame_download_rgb8.argtypes = [vp, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
         L.rt_frame_shard_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+        L.rt_rand_seed.argtypes = [C.POINTER(RandState), C.c_uint32]
+        L.rt_rand_seed.restype = None
+        L.rt_rand.argtypes = [C.POINTER(RandState)]
+        L.rt_rand.restype = C.c_int32
+        L.rt_lights_spherical.argtypes = [C.POINTER(Light), C.c_float, C.c_int32, C.POINTER(RandState), C.POINTER(Light)]
+        L.rt_lights_spherical.restype = C.c_int32
+        L.rt_light_directional.argtypes = [C.POINTER(Camera), C.POINTER(C.c_float * 3), C.POINTER(Light)]
+        L.rt_light_directional.restype = None
         L.rt_frame_shard_bytes.restype = C.c_int64
         L.rt_frame_pack_shard_rgb8.argtypes = [vp, vp]
         L.rt_frame_unpack_shards_rgb8.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32]
@@ -283,10 +298,12 @@ class Scene:
 
     @staticmethod
     def _lights(lights):
+        """[(pos3, color3) | (vec3, color3, kind)] -> rt_light array"""
         arr = (Light * max(len(lights), 1))()
-        for i, (p, c) in enumerate(lights):
-            arr[i].position[:] = list(p)
-            arr[i].color[:] = list(c)
+        for i, l in enumerate(lights):
+            arr[i].position[:] = list(l[0])
+            arr[i].color[:] = list(l[1])
+            arr[i].kind = l[2] if len(l) > 2 else RT_LIGHT_POINT
         return arr
 
     def render(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0, want_hits=False):
@@ -357,6 +374,38 @@ def write_ppm(path, rgb):
 def set_variant(v):
     """Kernel-variant override (A/B and tests); returns the previous value."""
     return lib().rt_debug_set_variant(int(v))
+
+
+class Rand:
+    """glibc rand() (the reference's unseeded rand(): seed 1)"""
+
+    def __init__(self, seed=1):
+        self.st = RandState()
+        lib().rt_rand_seed(C.byref(self.st), seed)
+
+    def __call__(self):
+        return lib().rt_rand(C.byref(self.st))
+
+
+def spherical_light(pos, color, radius, n_points, rng=None):
+    """Flyscene::sphericalLight + addLight('s'): n_points jittered lights then the centre, as
+    [(pos3, color3), ...] point lights."""
+    c = Light()
+    c.position[:] = list(pos)
+    c.color[:] = list(color)
+    out = (Light * (n_points + 1))()
+    n = lib().rt_lights_spherical(C.byref(c), radius, n_points, C.byref(rng.st) if rng else None, out)
+    if n < 0:
+        check(n)
+    return [(tuple(out[i].position), tuple(out[i].color)) for i in range(n)]
+
+
+def directional_light(cam, color):
+    """addLight('d'): (vector3, color3, RT_LIGHT_DIRECTIONAL) with the reference's stored vector."""
+    col = (C.c_float * 3)(*color)
+    out = Light()
+    lib().rt_light_directional(C.byref(cam), C.byref(col), C.byref(out))
+    return (tuple(out.position), tuple(out.color), RT_LIGHT_DIRECTIONAL)
 
 
 def shard_bytes(W, H, n):

@@ -295,3 +295,21 @@ def test_shard_pack_gather_unpack(rt, soup):
         torch.cuda.synchronize()
         rt.unpack_shards_rgb8(packed.data_ptr(), n, W, H, frame.data_ptr(), torch.cuda.current_device())
         np.testing.assert_array_equal(frame.cpu().numpy().reshape(H, W, 3), ref)
+
+
+def test_spherical_and_directional_lights(rt, orc):
+    """f4: a spherical light (jittered point lights from the reference's rand() sequence) plus a
+    directional light (the reference's stored screen-centre vector), FULL and PRIMARY, against the oracle."""
+    W, H = 480, 270
+    cam = rt.flycam(W, H, 0, 0, 20)
+    sph = rt.spherical_light((-0.5, 2.0, 3.0), (1.0, 1.0, 1.0), 0.4, 5, rng=rt.Rand(1))
+    dl = rt.directional_light(cam, (0.3, 0.25, 0.2))
+    lights = sph + [dl]
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    osc = orc.Scene(orc.Mesh.load_obj(scene_path("bunny.obj")))
+    for full in (False, True):
+        rgb, face, t, _ = sc.render(cam, lights, W, H, mode=rt.RT_MODE_FULL if full else rt.RT_MODE_PRIMARY,
+                                    want_hits=True)
+        orgb, oface, ot = osc.render(orc.flycam(W, H, 0, 0, 20), sph, W, H, full=full, threads=16,
+                                     dir_lights=[(dl[0], dl[1])])
+        compare(rgb, face, t, orgb, oface, ot, f"bunny-lights-{full}")

@@ -200,3 +200,46 @@ def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
     v = np.minimum(255, (np.float32(255) * rgb).astype(np.int64)).astype(np.uint8)
     rt.write_ppm_rgb8(b, v)
     assert a.read_bytes() == b.read_bytes()
+
+
+def test_rand_matches_glibc(rt):
+    """f4: rt_rand reproduces the C library's rand() the reference calls (glibc, unseeded = seed 1)."""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    for seed in (1, 12345, 0xFFFFFFFF):
+        libc.srand(ctypes.c_uint(seed))
+        ref = [libc.rand() for _ in range(2000)]
+        r = rt.Rand(seed)
+        assert [r() for _ in range(2000)] == ref, seed
+
+
+def test_spherical_light_expansion(rt):
+    """f4: sphericalLight + addLight('s') restated in float32 with the same rand() sequence."""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(ctypes.c_uint(1))
+    pos, col, radius, n = (0.3, -1.25, 2.5), (0.9, 0.6, 0.3), 0.35, 6
+    got = rt.spherical_light(pos, col, radius, n, rng=rt.Rand(1))
+    f = np.float32
+    q = f(2147483647) / (f(radius) * f(2))
+    div = f(n + 1)
+    for i in range(n):
+        off = [-f(radius) + (f(libc.rand()) / q) for _ in range(3)]
+        exp = tuple(f(pos[k]) + off[k] for k in range(3))
+        assert np.array_equal(np.array(got[i][0], f), np.array(exp, f)), i
+        assert np.array_equal(np.array(got[i][1], f), np.array(col, f) / div)
+    assert np.array_equal(np.array(got[n][0], f), np.array(pos, f))
+    assert len(got) == n + 1
+
+
+def test_directional_light_is_screen_centre(rt, orc):
+    """f4: addLight('d') stores screenToWorld(viewport centre): normalising (that - eye) gives the oracle's
+    primary-ray direction of the centre pixel bit for bit."""
+    for W, H, dz in ((1920, 1080, 20), (256, 256, 0)):
+        cam = rt.flycam(W, H, 0, 0, dz)
+        v, _, kind = rt.directional_light(cam, (1, 1, 1))
+        assert kind == rt.RT_LIGHT_DIRECTIONAL
+        o, d = orc.camera_ray(orc.flycam(W, H, 0, 0, dz), W // 2, H // 2)
+        diff = np.array(v, np.float32) - np.array(o, np.float32)
+        n = np.float32(np.sqrt(np.float32(diff[0] * diff[0] + (diff[1] * diff[1] + diff[2] * diff[2]))))
+        assert np.array_equal((diff / n).astype(np.float32), np.array(d, np.float32))
