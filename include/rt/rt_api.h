@@ -119,6 +119,10 @@ typedef struct rt_scene_info {
   int64_t device_bytes;
   double build_ms;        /* host preparation (boxes + BVH) */
   int32_t device;         /* RT_DEVICE_NONE for host-only scenes */
+  double prep_ms;         /* phases of rt_scene_create: per-vertex / per-face invariants, */
+  double boxes_ms;        /* the reference box partition, */
+  double bvh_ms;          /* the BVH build(s), */
+  double upload_ms;       /* the device upload */
 } rt_scene_info;
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);

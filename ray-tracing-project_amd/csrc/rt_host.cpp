@@ -508,11 +508,14 @@ extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
 // =====================================================================================================
 namespace rt {
 namespace {
+// The partition is a sequence of passes; within a pass every box that still qualifies is split (with
+// axis retries) independently of the others, and the boxes it creates are appended in box order. So a
+// pass runs its boxes in parallel and appends the results in order: the same boxes, face lists and
+// order as the sequential reference loop. Vertex coordinates are copied per face (9 floats, face
+// order) so the passes stream instead of gathering from the shared vertex array.
 struct BoxBuilder {
-  const float* v4;
-  const uint32_t* f;
-  std::vector<RefBox>& boxes;
-  const float* V(int32_t face, int k) const { return v4 + 4 * (size_t)f[3 * (size_t)face + k]; }
+  const float* fv;  // [nf][3 vertices][3] object-space coordinates (v / w is not taken: Tucano uses x,y,z)
+  const float* V(int32_t face, int k) const { return fv + 9 * (size_t)face + 3 * k; }
 
   static void reshape(RefBox& b) { for (int k = 0; k < 3; k++) b.shape[k] = b.high[k] - b.low[k]; }
 
@@ -550,9 +553,8 @@ struct BoxBuilder {
     avg /= (float)(b.faces.size() * 3);
     return avg;
   }
-  // splitBox: 1 = split into a new box, 0 = axis failed (returned `this`), -1 = nullptr
-  int split(size_t bi) {
-    RefBox& b = boxes[bi];
+  // splitBox: 1 = split, `out` receives the new box; 0 = axis failed (returned `this`); -1 = nullptr
+  int split(RefBox& b, RefBox& out) const {
     float oldLow[3], oldHigh[3];
     memcpy(oldLow, b.low, 12);
     memcpy(oldHigh, b.high, 12);
@@ -577,11 +579,10 @@ struct BoxBuilder {
     }
     b.faces = std::move(inside);
     b.failed[0] = b.failed[1] = b.failed[2] = false;
-    RefBox nb;
-    nb.faces = std::move(outside);
-    boxes.push_back(std::move(nb));  // invalidates b
-    fit(boxes.back());
-    fit(boxes[bi]);
+    out = RefBox();
+    out.faces = std::move(outside);
+    fit(out);
+    fit(b);
     return 1;
   }
 };
@@ -589,24 +590,51 @@ struct BoxBuilder {
 
 void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes) {
   hs.boxes.clear();
-  BoxBuilder bb{v4, hs.fidx.data(), hs.boxes};
+  std::vector<float> fv(9 * (size_t)hs.nf);
+  for (int32_t f = 0; f < hs.nf; f++)
+    for (int k = 0; k < 3; k++) memcpy(&fv[9 * (size_t)f + 3 * k], v4 + 4 * (size_t)hs.fidx[3 * (size_t)f + k], 12);
+  BoxBuilder bb{fv.data()};
   RefBox b0;
   b0.faces.resize(hs.nf);
   for (int32_t i = 0; i < hs.nf; i++) b0.faces[i] = i;
   hs.boxes.push_back(std::move(b0));
   bb.fit(hs.boxes[0]);
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   bool notDone = true;
   while (notDone && (int64_t)hs.boxes.size() < (int64_t)max_boxes) {
     notDone = false;
     const size_t ncur = hs.boxes.size();
+    std::vector<size_t> todo;
     for (size_t bi = 0; bi < ncur; bi++) {
-      RefBox& b = hs.boxes[bi];
-      if ((int64_t)b.faces.size() > min_faces && (!b.failed[0] || !b.failed[1] || !b.failed[2])) {
-        int r = bb.split(bi);
-        while (r == 0) r = bb.split(bi);
-        notDone = true;
-      }
+      const RefBox& b = hs.boxes[bi];
+      if ((int64_t)b.faces.size() > min_faces && (!b.failed[0] || !b.failed[1] || !b.failed[2])) todo.push_back(bi);
     }
+    if (todo.empty()) break;
+    notDone = true;
+    std::vector<RefBox> created(todo.size());
+    std::vector<char> made(todo.size(), 0);
+    auto work = [&](size_t i) {
+      RefBox& b = hs.boxes[todo[i]];
+      int r = bb.split(b, created[i]);
+      while (r == 0) r = bb.split(b, created[i]);
+      made[i] = r == 1;
+    };
+    // larger boxes first across the workers (the first passes hold few, huge boxes)
+    std::atomic<size_t> cursor{0};
+    std::vector<size_t> order(todo.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+      return hs.boxes[todo[a]].faces.size() > hs.boxes[todo[b]].faces.size();
+    });
+    const unsigned nth = (unsigned)std::min<size_t>(hw, todo.size());
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nth; t++)
+      th.emplace_back([&]() { for (size_t k; (k = cursor.fetch_add(1)) < order.size();) work(order[k]); });
+    for (size_t k; (k = cursor.fetch_add(1)) < order.size();) work(order[k]);
+    for (auto& t : th) t.join();
+    // the reference appends each new box right after splitting, i.e. in box order within the pass
+    for (size_t i = 0; i < todo.size(); i++)
+      if (made[i]) hs.boxes.push_back(std::move(created[i]));
   }
   hs.face_rank.assign(hs.nf, 0);
   hs.face_box.assign(hs.nf, 0);
@@ -624,13 +652,17 @@ void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t 
 // (rounded) triangle test: a triangle the reference accepts is never behind a culled box.
 // =====================================================================================================
 namespace {
-struct Prim { float lo[3], hi[3], c[3]; };
+struct Prim {
+  float lo[3], hi[3], c[3];
+  uint32_t id;  // face index
+};
 struct Aabb {
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   void grow(const float* l, const float* h) {
     for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], l[k]); hi[k] = std::max(hi[k], h[k]); }
   }
   void growp(const float* p) { grow(p, p); }
+  void merge(const Aabb& o) { grow(o.lo, o.hi); }
   float area() const {
     float d[3];
     for (int k = 0; k < 3; k++) d[k] = std::max(0.0f, hi[k] - lo[k]);
@@ -638,13 +670,17 @@ struct Aabb {
   }
 };
 
+// Binned SAH over the working array of primitives (partitioned in place, so a subtree's primitives are
+// contiguous and become the leaf order). Large ranges bin and bound in parallel chunks (min/max/count
+// merges are order-independent, so the splits do not depend on the thread count); subtrees above
+// 16k primitives build as separate tasks.
 struct BvhBuilder {
-  const std::vector<Prim>& prims;
-  std::vector<uint32_t>& idx;
+  std::vector<Prim>& prims;
   std::vector<Node64>& nodes;
   std::atomic<uint32_t> next{0};
   int leaf_size;
   float pad;
+  unsigned hw = 1;
   std::atomic<int> max_depth{0}, leaves{0};
   static constexpr int kBins = 32;
   static constexpr float kIsect = 1.0f;
@@ -662,12 +698,37 @@ struct BvhBuilder {
     }
   }
 
+  // run f(chunk_begin, chunk_end, chunk_index) over [b, e) in up to `hw` parallel chunks
+  template <typename F>
+  int chunked(uint32_t b, uint32_t e, F&& f) const {
+    const uint32_t n = e - b;
+    const int T = n >= 65536 ? (int)std::min<unsigned>(hw, 16) : 1;
+    if (T == 1) { f(b, e, 0); return 1; }
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++)
+      th.emplace_back([&, t]() { f(b + (uint32_t)((uint64_t)n * t / T), b + (uint32_t)((uint64_t)n * (t + 1) / T), t); });
+    f(b, b + (uint32_t)((uint64_t)n / T), 0);
+    for (auto& x : th) x.join();
+    return T;
+  }
+
+  struct Bins {
+    Aabb box[3][kBins];
+    uint32_t cnt[3][kBins];
+  };
+
   // builds [b,e); returns the handle and the (unpadded) bounds of the subtree
   uint32_t build(uint32_t b, uint32_t e, int depth, Aabb& box) {
-    Aabb cb;
-    box = Aabb();
-    for (uint32_t i = b; i < e; i++) { box.grow(prims[idx[i]].lo, prims[idx[i]].hi); cb.growp(prims[idx[i]].c); }
     const uint32_t n = e - b;
+    Aabb cb;
+    {
+      Aabb pb[16], pc[16];
+      const int T = chunked(b, e, [&](uint32_t lo, uint32_t hi, int t) {
+        for (uint32_t i = lo; i < hi; i++) { pb[t].grow(prims[i].lo, prims[i].hi); pc[t].growp(prims[i].c); }
+      });
+      box = Aabb();
+      for (int t = 0; t < T; t++) { box.merge(pb[t]); cb.merge(pc[t]); }
+    }
     int md = max_depth.load();
     while (depth > md && !max_depth.compare_exchange_weak(md, depth)) {}
     auto make_leaf_h = [&]() { leaves++; return make_leaf(b, n); };
@@ -681,32 +742,44 @@ struct BvhBuilder {
     const bool force_median = depth >= kMaxDepth - 20;
     if (!force_median) {
       int best_bin = -1;
+      float sc[3];
+      for (int k = 0; k < 3; k++) sc[k] = ext[k] > 0.0f ? kBins / ext[k] : 0.0f;
+      // one pass bins all three axes
+      std::vector<Bins> part(n >= 65536 ? std::min<unsigned>(hw, 16) : 1);
+      for (Bins& pbn : part) memset(pbn.cnt, 0, sizeof pbn.cnt);
+      const int T = chunked(b, e, [&](uint32_t lo, uint32_t hi, int t) {
+        Bins& B = part[t];
+        for (uint32_t i = lo; i < hi; i++) {
+          const Prim& p = prims[i];
+          for (int k = 0; k < 3; k++) {
+            if (!(ext[k] > 0.0f)) continue;
+            const int bi = std::min(kBins - 1, (int)((p.c[k] - cb.lo[k]) * sc[k]));
+            B.box[k][bi].grow(p.lo, p.hi);
+            B.cnt[k][bi]++;
+          }
+        }
+      });
+      for (int t = 1; t < T; t++)
+        for (int k = 0; k < 3; k++)
+          for (int i = 0; i < kBins; i++) { part[0].box[k][i].merge(part[t].box[k][i]); part[0].cnt[k][i] += part[t].cnt[k][i]; }
+      const Bins& bins = part[0];
       for (int k = 0; k < 3; k++) {
         if (!(ext[k] > 0.0f)) continue;
-        Aabb bins[kBins];
-        uint32_t cnt[kBins] = {0};
-        const float sc = kBins / ext[k];
-        for (uint32_t i = b; i < e; i++) {
-          const Prim& p = prims[idx[i]];
-          int bi = std::min(kBins - 1, (int)((p.c[k] - cb.lo[k]) * sc));
-          bins[bi].grow(p.lo, p.hi);
-          cnt[bi]++;
-        }
         float right_area[kBins];
         uint32_t right_cnt[kBins];
         Aabb acc;
         uint32_t c = 0;
         for (int i = kBins - 1; i > 0; i--) {
-          acc.grow(bins[i].lo, bins[i].hi);
-          c += cnt[i];
+          acc.merge(bins.box[k][i]);
+          c += bins.cnt[k][i];
           right_area[i] = acc.area();
           right_cnt[i] = c;
         }
         Aabb lacc;
         uint32_t lc = 0;
         for (int i = 0; i < kBins - 1; i++) {
-          lacc.grow(bins[i].lo, bins[i].hi);
-          lc += cnt[i];
+          lacc.merge(bins.box[k][i]);
+          lc += bins.cnt[k][i];
           if (lc == 0 || right_cnt[i + 1] == 0) continue;
           float cost = lacc.area() * lc + right_area[i + 1] * right_cnt[i + 1];
           if (cost < best_cost) { best_cost = cost; axis = k; best_bin = i; }
@@ -716,12 +789,12 @@ struct BvhBuilder {
       const float split_cost = kTrav + kIsect * best_cost / parent_area;
       if ((int)n <= leaf_size && (axis < 0 || (float)n * kIsect <= split_cost)) return make_leaf_h();
       if (axis >= 0) {
-        const float sc = kBins / ext[axis];
+        const float s = sc[axis];
         const float lo = cb.lo[axis];
-        auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t pi) {
-          return std::min(kBins - 1, (int)((prims[pi].c[axis] - lo) * sc)) <= best_bin;
+        auto it = std::partition(prims.begin() + b, prims.begin() + e, [&](const Prim& p) {
+          return std::min(kBins - 1, (int)((p.c[axis] - lo) * s)) <= best_bin;
         });
-        mid = (uint32_t)(it - idx.begin());
+        mid = (uint32_t)(it - prims.begin());
       }
     } else if ((int)n <= leaf_size) {
       return make_leaf_h();
@@ -731,13 +804,13 @@ struct BvhBuilder {
       if ((int)n <= kMaxLeaf && !(ext[0] > 0 || ext[1] > 0 || ext[2] > 0)) return make_leaf_h();
       int k = (ext[0] >= ext[1] && ext[0] >= ext[2]) ? 0 : (ext[1] >= ext[2] ? 1 : 2);
       mid = b + n / 2;
-      std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e,
-                       [&](uint32_t x, uint32_t y) { return prims[x].c[k] < prims[y].c[k]; });
+      std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e,
+                       [&](const Prim& x, const Prim& y) { return x.c[k] < y.c[k]; });
     }
     const uint32_t me = next.fetch_add(1);
     Aabb lb, rb;
     uint32_t lh, rh;
-    if (n > 65536 && depth < 4) {
+    if (n > 4096 && depth < 16) {
       auto fut = std::async(std::launch::async, [&]() { return build(b, mid, depth + 1, lb); });
       rh = build(mid, e, depth + 1, rb);
       lh = fut.get();
@@ -753,6 +826,17 @@ struct BvhBuilder {
   }
 };
 }  // namespace
+
+// f(begin, end, chunk) over [0, n) in hardware_concurrency() contiguous chunks (one when n is small)
+template <typename F>
+static int parallel_chunks(size_t n, F&& f) {
+  const int T = n >= 65536 ? (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1;
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back([&, t]() { f(n * t / T, n * (t + 1) / T, t); });
+  f(0, n / T, 0);
+  for (auto& x : th) x.join();
+  return T;
+}
 
 // A face whose interpolated normal (interpolateNormal, flyscene.cpp:594-599) can never be the zero
 // vector for a point that passed the inside test: its area A (same expression the kernel uses) is a
@@ -784,18 +868,23 @@ void build_bvh(HostScene& hs, int leaf_size) {
   hs.leaves = 0;
   if (hs.nf == 0) { hs.root = 0; return; }
   std::vector<Prim> prims(hs.nf);
-  Aabb world;
-  for (int32_t f = 0; f < hs.nf; f++) {
-    Prim& p = prims[f];
-    for (int k = 0; k < 3; k++) { p.lo[k] = INFINITY; p.hi[k] = -INFINITY; }
-    for (int j = 0; j < 3; j++) {
-      const f3& w = hs.wv[hs.fidx[3 * f + j]];
-      const float c[3] = {w.x, w.y, w.z};
-      for (int k = 0; k < 3; k++) { p.lo[k] = std::min(p.lo[k], c[k]); p.hi[k] = std::max(p.hi[k], c[k]); }
+  Aabb wparts[16];
+  const int TW = parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int t) {
+    for (size_t f = b; f < e; f++) {
+      Prim& p = prims[f];
+      p.id = (uint32_t)f;
+      for (int k = 0; k < 3; k++) { p.lo[k] = INFINITY; p.hi[k] = -INFINITY; }
+      for (int j = 0; j < 3; j++) {
+        const f3& w = hs.wv[hs.fidx[3 * f + j]];
+        const float c[3] = {w.x, w.y, w.z};
+        for (int k = 0; k < 3; k++) { p.lo[k] = std::min(p.lo[k], c[k]); p.hi[k] = std::max(p.hi[k], c[k]); }
+      }
+      for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.lo[k] + p.hi[k]);
+      wparts[t].grow(p.lo, p.hi);
     }
-    for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.lo[k] + p.hi[k]);
-    world.grow(p.lo, p.hi);
-  }
+  });
+  Aabb world;
+  for (int t = 0; t < TW; t++) world.merge(wparts[t]);
   float ext = 0.0f, mag = 0.0f;
   for (int k = 0; k < 3; k++) {
     ext = std::max(ext, world.hi[k] - world.lo[k]);
@@ -804,15 +893,17 @@ void build_bvh(HostScene& hs, int leaf_size) {
   // conservative padding: covers the reference's rounding of P = o + t d and of the inclusive edge
   // tests for ray origins within ~16 scene extents (DESIGN.md "Exactness of culling")
   const float pad = 2e-5f * std::max(std::max(ext, mag), 1e-3f);
-  std::vector<uint32_t> idx(hs.nf);
-  for (int32_t f = 0; f < hs.nf; f++) idx[f] = (uint32_t)f;
   std::vector<Node64> tmp((size_t)std::max(hs.nf, 1));
-  BvhBuilder B{prims, idx, tmp};
+  BvhBuilder B{prims, tmp};
+  B.hw = std::max(1u, std::thread::hardware_concurrency());
   B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
   if (const char* e = getenv("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
   B.pad = pad;
   Aabb rootb;
+  const bool timing = getenv("RT_TIMING") != nullptr;
+  auto tb0 = std::chrono::steady_clock::now();
   uint32_t root = B.build(0, (uint32_t)hs.nf, 0, rootb);
+  if (timing) fprintf(stderr, "[rt] bvh recursive build %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
   uint32_t nn = B.next.load();
   if (is_leaf(root)) {  // whole scene in one leaf: wrap in a node whose second child never hits
     Node64 nd{};
@@ -849,8 +940,9 @@ void build_bvh(HostScene& hs, int leaf_size) {
   hs.leaves = B.leaves.load();
   // triangle records in leaf order
   hs.tris.resize(hs.nf);
-  for (int32_t s = 0; s < hs.nf; s++) {
-    const uint32_t f = idx[s];
+  parallel_chunks((size_t)hs.nf, [&](size_t sb, size_t se, int) {
+  for (size_t s = sb; s < se; s++) {
+    const uint32_t f = prims[s].id;
     TriRec64& r = hs.tris[s];
     const f3& n = hs.fnn[f];
     const f3& w0 = hs.wv[hs.fidx[3 * f]];
@@ -864,6 +956,7 @@ void build_bvh(HostScene& hs, int leaf_size) {
     r.face = f;
     r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u);
   }
+  });
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1036,9 +1129,17 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     hs.fnn[f] = rt::normalized(f3{n[0], n[1], n[2]});
     hs.fdist[f] = rt::dot(hs.fnn[f], hs.wv[hs.fidx[3 * f]]);
   }
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  s->prep_ms = ms_since(t0);
+  auto t1 = clk::now();
   rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
+  s->boxes_ms = ms_since(t1);
+  auto t2 = clk::now();
   rt::build_bvh(hs, leaf);
+  if (getenv("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));
   rt::build_bvh4(hs);
+  s->bvh_ms = ms_since(t2);
   if (3 * hs.depth4 + 4 > rt::kStack4) hs.nodes4.clear();  // too deep for the wide stack: binary traversal
   if (hs.depth > rt::kMaxDepth + 2) {  // the wave stack holds 64 entries
     delete s;
@@ -1047,8 +1148,10 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   }
   s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (s->opts.device != RT_DEVICE_NONE) {
+    auto t3 = clk::now();
     int rc = rt::device_upload(s);
     if (rc) { delete s; return rc; }
+    s->upload_ms = ms_since(t3);
   }
   *out = s;
   return RT_OK;
@@ -1071,6 +1174,10 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->device_bytes = s->device_bytes;
   o->build_ms = s->build_ms;
   o->device = s->device;
+  o->prep_ms = s->prep_ms;
+  o->boxes_ms = s->boxes_ms;
+  o->bvh_ms = s->bvh_ms;
+  o->upload_ms = s->upload_ms;
   return RT_OK;
 }
 

@@ -56,7 +56,7 @@ void set_error(const char* fmt, ...);
 struct rt_scene {
   rt_scene_opts opts;
   rt::HostScene hs;
-  double build_ms = 0.0;
+  double build_ms = 0.0, prep_ms = 0.0, boxes_ms = 0.0, bvh_ms = 0.0, upload_ms = 0.0;
   int32_t device = RT_DEVICE_NONE;
   // device state (rt_device.hip)
   void* stream = nullptr;        // = slots[0].stream (ray-list queries, uploads)

@@ -52,7 +52,8 @@ class SceneOpts(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("n_faces", C.c_int32), ("n_vertices", C.c_int32), ("n_ref_boxes", C.c_int32),
                 ("bvh_nodes", C.c_int32), ("bvh_leaves", C.c_int32), ("bvh_depth", C.c_int32),
-                ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("device", C.c_int32)]
+                ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("device", C.c_int32),
+                ("prep_ms", C.c_double), ("boxes_ms", C.c_double), ("bvh_ms", C.c_double), ("upload_ms", C.c_double)]
 
 
 class Camera(C.Structure):
