@@ -175,6 +175,8 @@ def main():
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + 8-bit frame to host) timing")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
+    ap.add_argument("--builder", choices=["sah", "lbvh"], default="sah",
+                    help="BVH builder: host binned SAH (default) or the device LBVH (SURVEY f2)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames that may overlap on the GPU (0 = library default, 3)")
     a = ap.parse_args()
@@ -217,7 +219,8 @@ def main():
     else:
         mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         scene_name = "Stanford bunny (69,451 triangles)"
-    sc = rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight)
+    sc = rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight,
+                  builder=rt.RT_BUILDER_LBVH_GPU if a.builder == "lbvh" else rt.RT_BUILDER_SAH)
     info = sc.info()
     info_fif = a.frames_in_flight or 3
     setup_s = time.perf_counter() - t0
@@ -325,7 +328,11 @@ def main():
                        "trace_kernel_ms": round(trace_ms_max, 4),
                        "kernel_mrays_per_s": round(total_rays / a.steps / (kernel_ms_max * 1e-3) / 1e6, 2),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
-                       "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2), **extra},
+                       "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
+                       "builder": "lbvh-gpu" if info["builder"] == 1 else "sah-host",
+                       "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
+                                    "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),
+                                    "upload": round(info["upload_ms"], 1)}, **extra},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

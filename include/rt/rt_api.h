@@ -102,7 +102,13 @@ typedef struct rt_scene_opts {
   int32_t frames_in_flight; /* rt_render_async frames that may execute concurrently (1..4, default 3):
                              * each in-flight frame has its own stream and frame buffers; frames stay
                              * independent and rt_frame_download returns the most recent one */
+  int32_t builder;          /* RT_BUILDER_SAH (host binned SAH, default: fastest traversal) or
+                             * RT_BUILDER_LBVH_GPU (Morton/radix-sort/Karras build on the
+                             * device in milliseconds; falls back to SAH when the tree would be too deep) */
 } rt_scene_opts;
+
+#define RT_BUILDER_SAH 0
+#define RT_BUILDER_LBVH_GPU 1
 
 void rt_scene_opts_default(rt_scene_opts* o);
 
@@ -123,6 +129,8 @@ typedef struct rt_scene_info {
   double boxes_ms;        /* the reference box partition, */
   double bvh_ms;          /* the BVH build(s), */
   double upload_ms;       /* the device upload */
+  int32_t builder;        /* the builder actually used (RT_BUILDER_*) */
+  double bvh_gpu_ms;      /* device time of the LBVH kernels (RT_BUILDER_LBVH_GPU) */
 } rt_scene_info;
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);

@@ -1234,6 +1234,13 @@ static int dalloc_copy(T** dst, const void* src, size_t bytes, int64_t& total) {
   return RT_OK;
 }
 
+int current_device() {
+  int ndev = 0, dev = -1;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -1;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  return dev;
+}
+
 int device_upload(rt_scene* s) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {

@@ -861,6 +861,81 @@ static bool safe_normal(const HostScene& hs, uint32_t f) {
   return true;
 }
 
+// conservative padding of every BVH child box: covers the reference's rounding of P = o + t d and of
+// the inclusive edge tests for ray origins within ~16 scene extents (DESIGN.md "Exactness of culling")
+static float bvh_pad(const float lo[3], const float hi[3]) {
+  float ext = 0.0f, mag = 0.0f;
+  for (int k = 0; k < 3; k++) {
+    ext = std::max(ext, hi[k] - lo[k]);
+    mag = std::max(mag, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
+  }
+  return 2e-5f * std::max(std::max(ext, mag), 1e-3f);
+}
+
+void world_bounds(const HostScene& hs, float lo[3], float hi[3]) {
+  Aabb parts[16];
+  const int T = parallel_chunks((size_t)hs.nv, [&](size_t b, size_t e, int t) {
+    for (size_t i = b; i < e; i++) {
+      const float c[3] = {hs.wv[i].x, hs.wv[i].y, hs.wv[i].z};
+      parts[t].growp(c);
+    }
+  });
+  Aabb w;
+  for (int t = 0; t < T; t++) w.merge(parts[t]);
+  for (int k = 0; k < 3; k++) { lo[k] = w.lo[k]; hi[k] = w.hi[k]; }
+}
+
+// exact-test record of face f (the kernels' TriRec64)
+static void tri_record(const HostScene& hs, uint32_t f, TriRec64& r) {
+  const f3& n = hs.fnn[f];
+  const f3& w0 = hs.wv[hs.fidx[3 * f]];
+  const f3& w1 = hs.wv[hs.fidx[3 * f + 1]];
+  const f3& w2 = hs.wv[hs.fidx[3 * f + 2]];
+  r.nx = n.x; r.ny = n.y; r.nz = n.z; r.dist = hs.fdist[f];
+  r.w0x = w0.x; r.w0y = w0.y; r.w0z = w0.z;
+  r.w1x = w1.x; r.w1y = w1.y; r.w1z = w1.z;
+  r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
+  r.rank = hs.face_rank[f];
+  r.face = f;
+  r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u);
+}
+
+void face_records(const HostScene& hs, std::vector<TriRec64>& out) {
+  out.resize(hs.nf);
+  parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int) {
+    for (size_t f = b; f < e; f++) tri_record(hs, (uint32_t)f, out[f]);
+  });
+}
+
+// interior nodes re-laid out depth-first (near child first) from `root`; unreferenced nodes dropped;
+// sets hs.nodes, hs.root = 0, hs.depth (levels of interior nodes + the leaf level)
+void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) {
+  std::vector<uint32_t> remap(tmp.size(), UINT32_MAX), order;
+  std::vector<std::pair<uint32_t, int>> st{{root, 1}};
+  int depth = 0;
+  while (!st.empty()) {
+    const auto [n, d] = st.back();
+    st.pop_back();
+    remap[n] = (uint32_t)order.size();
+    order.push_back(n);
+    depth = std::max(depth, d + 1);
+    const Node64& nd = tmp[n];
+    if (!is_leaf(nd.child1)) st.push_back({nd.child1, d + 1});
+    if (!is_leaf(nd.child0)) st.push_back({nd.child0, d + 1});
+  }
+  hs.nodes.resize(order.size());
+  for (size_t i = 0; i < order.size(); i++) {
+    Node64 nd = tmp[order[i]];
+    if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
+    if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
+    hs.nodes[i] = nd;
+  }
+  hs.root = 0;
+  hs.depth = depth;
+  hs.leaves = 0;
+  for (const Node64& nd : hs.nodes) hs.leaves += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
+}
+
 void build_bvh(HostScene& hs, int leaf_size) {
   hs.nodes.clear();
   hs.tris.clear();
@@ -885,20 +960,12 @@ void build_bvh(HostScene& hs, int leaf_size) {
   });
   Aabb world;
   for (int t = 0; t < TW; t++) world.merge(wparts[t]);
-  float ext = 0.0f, mag = 0.0f;
-  for (int k = 0; k < 3; k++) {
-    ext = std::max(ext, world.hi[k] - world.lo[k]);
-    mag = std::max(mag, std::max(std::fabs(world.lo[k]), std::fabs(world.hi[k])));
-  }
-  // conservative padding: covers the reference's rounding of P = o + t d and of the inclusive edge
-  // tests for ray origins within ~16 scene extents (DESIGN.md "Exactness of culling")
-  const float pad = 2e-5f * std::max(std::max(ext, mag), 1e-3f);
   std::vector<Node64> tmp((size_t)std::max(hs.nf, 1));
   BvhBuilder B{prims, tmp};
   B.hw = std::max(1u, std::thread::hardware_concurrency());
   B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
   if (const char* e = getenv("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
-  B.pad = pad;
+  B.pad = bvh_pad(world.lo, world.hi);
   Aabb rootb;
   const bool timing = getenv("RT_TIMING") != nullptr;
   auto tb0 = std::chrono::steady_clock::now();
@@ -915,48 +982,38 @@ void build_bvh(HostScene& hs, int leaf_size) {
     nn = 1;
     root = 0;
   }
-  // re-layout interior nodes in depth-first (near child first) order
-  hs.nodes.resize(nn);
-  std::vector<uint32_t> remap(nn, UINT32_MAX), order;
-  order.reserve(nn);
-  std::vector<uint32_t> st{root};
-  while (!st.empty()) {
-    uint32_t n = st.back();
-    st.pop_back();
-    remap[n] = (uint32_t)order.size();
-    order.push_back(n);
-    const Node64& nd = tmp[n];
-    if (!is_leaf(nd.child1)) st.push_back(nd.child1);
-    if (!is_leaf(nd.child0)) st.push_back(nd.child0);
-  }
-  for (uint32_t i = 0; i < nn; i++) {
-    Node64 nd = tmp[order[i]];
-    if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
-    if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
-    hs.nodes[i] = nd;
-  }
-  hs.root = 0;
-  hs.depth = B.max_depth.load() + 1;
+  tmp.resize(nn);
+  relayout_dfs(hs, tmp, root);
   hs.leaves = B.leaves.load();
   // triangle records in leaf order
   hs.tris.resize(hs.nf);
   parallel_chunks((size_t)hs.nf, [&](size_t sb, size_t se, int) {
-  for (size_t s = sb; s < se; s++) {
-    const uint32_t f = prims[s].id;
-    TriRec64& r = hs.tris[s];
-    const f3& n = hs.fnn[f];
-    const f3& w0 = hs.wv[hs.fidx[3 * f]];
-    const f3& w1 = hs.wv[hs.fidx[3 * f + 1]];
-    const f3& w2 = hs.wv[hs.fidx[3 * f + 2]];
-    r.nx = n.x; r.ny = n.y; r.nz = n.z; r.dist = hs.fdist[f];
-    r.w0x = w0.x; r.w0y = w0.y; r.w0z = w0.z;
-    r.w1x = w1.x; r.w1y = w1.y; r.w1z = w1.z;
-    r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
-    r.rank = hs.face_rank[f];
-    r.face = f;
-    r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u);
-  }
+    for (size_t s = sb; s < se; s++) tri_record(hs, prims[s].id, hs.tris[s]);
   });
+}
+
+// GPU LBVH (rt_build.hip) + host depth-first re-layout; false (with nothing changed) if the device
+// build is not possible, in which case the caller builds on the host
+bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
+  if (hs.nf <= leaf_size || hs.nf < 2) return false;
+  float lo[3], hi[3];
+  world_bounds(hs, lo, hi);
+  std::vector<TriRec64> recs;
+  face_records(hs, recs);
+  std::vector<Node64> tmp;
+  std::vector<TriRec64> tris;
+  if (gpu_build_lbvh(device, recs, lo, hi, std::max(1, std::min(leaf_size, kMaxLeaf)), bvh_pad(lo, hi), tmp, tris,
+                     gpu_ms) != RT_OK)
+    return false;
+  HostScene trial;
+  relayout_dfs(trial, tmp, 0);
+  if (trial.depth > kMaxDepth + 2) return false;  // too deep for the wave stack: host SAH instead
+  hs.nodes = std::move(trial.nodes);
+  hs.root = 0;
+  hs.depth = trial.depth;
+  hs.leaves = trial.leaves;
+  hs.tris = std::move(tris);
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1136,9 +1193,18 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
   s->boxes_ms = ms_since(t1);
   auto t2 = clk::now();
-  rt::build_bvh(hs, leaf);
-  if (getenv("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));
-  rt::build_bvh4(hs);
+  bool built = false;
+  if (s->opts.builder == RT_BUILDER_LBVH_GPU && s->opts.device != RT_DEVICE_NONE) {
+    int dev = s->opts.device;
+    if (dev < 0) dev = rt::current_device();
+    built = dev >= 0 && rt::build_bvh_gpu(hs, dev, leaf, &s->bvh_gpu_ms);
+    if (built) s->builder_used = RT_BUILDER_LBVH_GPU;
+  }
+  if (!built) {
+    rt::build_bvh(hs, leaf);
+    if (getenv("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));
+    rt::build_bvh4(hs);
+  }
   s->bvh_ms = ms_since(t2);
   if (3 * hs.depth4 + 4 > rt::kStack4) hs.nodes4.clear();  // too deep for the wide stack: binary traversal
   if (hs.depth > rt::kMaxDepth + 2) {  // the wave stack holds 64 entries
@@ -1178,6 +1244,8 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->boxes_ms = s->boxes_ms;
   o->bvh_ms = s->bvh_ms;
   o->upload_ms = s->upload_ms;
+  o->builder = s->builder_used;
+  o->bvh_gpu_ms = s->bvh_gpu_ms;
   return RT_OK;
 }
 

@@ -34,7 +34,7 @@ constexpr uint32_t kSafeNormalBit = 0x80000000u;
 RT_HD bool is_leaf(uint32_t h) { return (h & kLeafBit) != 0; }
 RT_HD uint32_t leaf_first(uint32_t h) { return h & kLeafFirstMask; }
 RT_HD uint32_t leaf_count(uint32_t h) { return ((h >> kLeafCountShift) & 15u) + 1u; }
-inline uint32_t make_leaf(uint32_t first, uint32_t count) {
+RT_HD uint32_t make_leaf(uint32_t first, uint32_t count) {
   return kLeafBit | ((count - 1u) << kLeafCountShift) | first;
 }
 

@@ -48,6 +48,9 @@ struct HostScene {
 
 void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes);
 void build_bvh(HostScene& hs, int leaf_size);
+bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms);
+int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
+                   int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
 void build_bvh4(HostScene& hs);
 void set_error(const char* fmt, ...);
 
@@ -56,7 +59,8 @@ void set_error(const char* fmt, ...);
 struct rt_scene {
   rt_scene_opts opts;
   rt::HostScene hs;
-  double build_ms = 0.0, prep_ms = 0.0, boxes_ms = 0.0, bvh_ms = 0.0, upload_ms = 0.0;
+  double build_ms = 0.0, prep_ms = 0.0, boxes_ms = 0.0, bvh_ms = 0.0, upload_ms = 0.0, bvh_gpu_ms = 0.0;
+  int32_t builder_used = 0;
   int32_t device = RT_DEVICE_NONE;
   // device state (rt_device.hip)
   void* stream = nullptr;        // = slots[0].stream (ray-list queries, uploads)
@@ -95,5 +99,6 @@ struct rt_scene {
 
 namespace rt {
 int device_upload(rt_scene* s);
+int current_device();  // -1 without a GPU
 void device_release(rt_scene* s);
 }  // namespace rt

@@ -313,3 +313,28 @@ def test_spherical_and_directional_lights(rt, orc):
         orgb, oface, ot = osc.render(orc.flycam(W, H, 0, 0, 20), sph, W, H, full=full, threads=16,
                                      dir_lights=[(dl[0], dl[1])])
         compare(rgb, face, t, orgb, oface, ot, f"bunny-lights-{full}")
+
+
+@pytest.mark.parametrize("name", ["bunny", "soup"])
+def test_gpu_lbvh_builder(rt, soup, name):
+    """f2: the device LBVH build gives a sound tree (host containment / coverage check) and the frame of
+    the host-SAH scene bit for bit (PRIMARY and FULL)."""
+    if name == "bunny":
+        mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
+        ref = rt.Scene(mesh)
+        W, H = 1920, 1080
+    else:
+        ref, _ = soup
+        mesh = ref.mesh
+        W, H = 960, 540
+    lb = rt.Scene(mesh, builder=rt.RT_BUILDER_LBVH_GPU)
+    info = lb.info()
+    assert info["builder"] == rt.RT_BUILDER_LBVH_GPU and info["bvh_gpu_ms"] > 0
+    v = lb.validate_bvh()
+    assert v["ok"] and v["covered2"] == info["n_faces"], v
+    cam = rt.flycam(W, H, 0, 0, 20)
+    for m in (rt.RT_MODE_PRIMARY, rt.RT_MODE_FULL):
+        a = ref.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        b = lb.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (name, m)
