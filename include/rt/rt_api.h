@@ -96,7 +96,7 @@ typedef struct rt_scene_opts {
   int32_t device;         /* HIP device ordinal; -1 = current device; RT_DEVICE_NONE = host only */
   int32_t min_faces;      /* Flyscene::MIN_FACES (flyscene.hpp:168), default 300 */
   int32_t max_boxes;      /* Flyscene::MAX_BOXES (flyscene.hpp:169), default INT32_MAX */
-  int32_t leaf_size;      /* BVH leaf size bound (1..16), 0 = default */
+  int32_t leaf_size;      /* BVH leaf size bound (1..16), 0 = default (4 for SAH, 1 for the GPU LBVH) */
   rt_material default_material; /* Flyscene::ka/kd/ks/shininess defaults (flyscene.hpp:179-184) */
   float background[3];    /* Flyscene::BACKGROUND_COLOR (flyscene.hpp:175) */
   int32_t frames_in_flight; /* rt_render_async frames that may execute concurrently (1..4, default 3):

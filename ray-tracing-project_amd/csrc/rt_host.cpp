@@ -1197,7 +1197,10 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   if (s->opts.builder == RT_BUILDER_LBVH_GPU && s->opts.device != RT_DEVICE_NONE) {
     int dev = s->opts.device;
     if (dev < 0) dev = rt::current_device();
-    built = dev >= 0 && rt::build_bvh_gpu(hs, dev, leaf, &s->bvh_gpu_ms);
+    // LBVH default leaf bound 1: the Morton tree's small subtrees are poor leaves (measured at 1M tris:
+    // 1 -> 97% of the SAH tree's traversal rate, 4 -> 85%)
+    const int lb_leaf = s->opts.leaf_size > 0 ? s->opts.leaf_size : 1;
+    built = dev >= 0 && rt::build_bvh_gpu(hs, dev, lb_leaf, &s->bvh_gpu_ms);
     if (built) s->builder_used = RT_BUILDER_LBVH_GPU;
   }
   if (!built) {
