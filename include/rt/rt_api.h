@@ -259,6 +259,24 @@ int rt_trace_closest(rt_scene* s, int32_t n, const float* origins3, const float*
                      float* t, float* P3);
 /* shadow(P, L) (flyscene.cpp:510-526) for n rays on the device: blocked 1/0 */
 int rt_trace_shadow(rt_scene* s, int32_t n, const float* P3, const float* L3, int32_t* blocked);
+/* calculateMinimumFace plus interpolateNormal at the hit (N [n][3], zero on a miss) */
+int rt_trace_closest_normal(rt_scene* s, int32_t n, const float* o3, const float* d3, int32_t* face, float* t,
+                            float* P3, float* N3);
+/* traceRay(o, d, 0) (flyscene.cpp:317-371, max_depth 2 with shadows: the FULL frame's colour path) for
+ * arbitrary rays: colour rgb [n][3], first-hit face (-1 miss) and t (NULL = skip). */
+int rt_trace_color(rt_scene* s, int32_t n, const float* o3, const float* d3, const rt_light* lights, int32_t n_lights,
+                   float* rgb3, int32_t* face, float* t);
+
+/* createDebugRay (flyscene.cpp:129-173) without the GL cylinders: the camera ray through a
+ * (float) mouse position and its reflection chain, up to max_depth segments; every segment carries the
+ * first ray's traceRay colour; a miss ends the chain with a 10-unit segment. *n_out = segments written. */
+typedef struct rt_ray_segment {
+  float origin[3], direction[3];
+  float length;
+  float color[3];
+} rt_ray_segment;
+int rt_debug_ray(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights, float mouse_x, float mouse_y,
+                 int32_t max_depth, rt_ray_segment* out, int32_t* n_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Misc

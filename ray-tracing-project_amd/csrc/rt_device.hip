@@ -779,22 +779,15 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
 
 // FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
 // bounce, all in one kernel (flyscene.cpp:317-371, 510-566, 603-614).
-#ifndef RT_FULL_WAVES_PER_EU
-#define RT_FULL_WAVES_PER_EU 8  // measured: 8 waves (64 VGPR + stack spill) beats 3 (150 VGPR) by 24% on C3 FULL
-#endif
-template <bool STATS, bool HITS, int TRAV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU)))
-void k_render_full(FrameParams P) {
-  __shared__ WaveLds<TRAV, STATS> lds;
-  const PixelCoord c = pixel_coord(P);
-  const bool active = c.active;
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
-  const Ray r = primary_ray(P, c.px, c.py);
-  if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
-
-  Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+// traceRay(o, d, 0) with max_depth 2 (FULL, flyscene.cpp:317-371): primary hit, per-light shadows, one
+// reflection bounce with its own shadows. Shared by the frame megakernel and the ray-list colour query.
+// Returns the colour; h0 / face0: the first hit (t, face id).
+template <bool STATS, int TRAV>
+__device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, bool active, WaveLds<TRAV, STATS>& lds, int wv,
+                                         uint32_t* cnt, Hit& h, uint32_t& face0) {
+  h = Hit{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  trace<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, c.wv, cnt);
+  trace<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
   const bool hit0 = active && h.t != INFINITY;
   if (STATS && hit0) cnt[ST_HITS]++;
 
@@ -810,7 +803,7 @@ void k_render_full(FrameParams P) {
     hi0.p = f3{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
     hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
   }
-  const f3 direct0 = calc_color<true, STATS, TRAV>(P, st, hi0, r.o, hit0, &lds, c.wv, cnt);
+  const f3 direct0 = calc_color<true, STATS, TRAV>(P, st, hi0, r.o, hit0, &lds, wv, cnt);
   if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
 
   // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
@@ -823,7 +816,7 @@ void k_render_full(FrameParams P) {
   setup_cull(rr);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  trace<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, c.wv, cnt);
+  trace<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
   hi1.mat = -1;
@@ -835,7 +828,7 @@ void k_render_full(FrameParams P) {
     hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
     hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
   }
-  const f3 direct1 = calc_color<true, STATS, TRAV>(P, st, hi1, rr.o, hit1, &lds, c.wv, cnt);
+  const f3 direct1 = calc_color<true, STATS, TRAV>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
   if (hit1) {
     if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
     // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
@@ -849,13 +842,34 @@ void k_render_full(FrameParams P) {
   } else {
     col = f3{P.bg[0], P.bg[1], P.bg[2]};
   }
+  face0 = hit0 ? hi0.face : 0xFFFFFFFFu;
+  return col;
+}
+
+#ifndef RT_FULL_WAVES_PER_EU
+#define RT_FULL_WAVES_PER_EU 8  // measured: 8 waves (64 VGPR + stack spill) beats 3 (150 VGPR) by 24% on C3 FULL
+#endif
+template <bool STATS, bool HITS, int TRAV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU)))
+void k_render_full(FrameParams P) {
+  __shared__ WaveLds<TRAV, STATS> lds;
+  const PixelCoord c = pixel_coord(P);
+  const bool active = c.active;
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  const Ray r = primary_ray(P, c.px, c.py);
+  if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
+
+  Hit h;
+  uint32_t face0;
+  const f3 col = trace_full<STATS, TRAV>(P, r, active, lds, c.wv, cnt, h, face0);
+  const bool hit0 = face0 != 0xFFFFFFFFu;
   if (active) {
     const size_t pix = (size_t)c.py * P.W + c.px;
     P.rgb[3 * pix + 0] = col.x;
     P.rgb[3 * pix + 1] = col.y;
     P.rgb[3 * pix + 2] = col.z;
     if (HITS) {
-      P.face_out[pix] = hit0 ? (int32_t)hi0.face : -1;
+      P.face_out[pix] = hit0 ? (int32_t)face0 : -1;
       P.t_out[pix] = h.t;
     }
   }
@@ -1150,16 +1164,53 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
     const TriRec64 tr = vload_tri(P.sc.tris, h.slot);
     R.face[i] = (int32_t)tr.face;
     R.t[i] = h.t;
+    const f3 p{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
     if (R.P) {
-      R.P[3 * (size_t)i + 0] = r.o.x + h.t * r.d.x;
-      R.P[3 * (size_t)i + 1] = r.o.y + h.t * r.d.y;
-      R.P[3 * (size_t)i + 2] = r.o.z + h.t * r.d.z;
+      R.P[3 * (size_t)i + 0] = p.x;
+      R.P[3 * (size_t)i + 1] = p.y;
+      R.P[3 * (size_t)i + 2] = p.z;
+    }
+    if (R.N) {  // interpolateNormal(face, P) (flyscene.cpp:572-600)
+      int32_t mat;
+      const f3 nn = hit_normal(P.sc, tr, p, mat);
+      R.N[3 * (size_t)i + 0] = nn.x;
+      R.N[3 * (size_t)i + 1] = nn.y;
+      R.N[3 * (size_t)i + 2] = nn.z;
     }
   } else {
     R.face[i] = -1;
     R.t[i] = INFINITY;
     if (R.P) R.P[3 * (size_t)i] = R.P[3 * (size_t)i + 1] = R.P[3 * (size_t)i + 2] = 0.0f;
+    if (R.N) R.N[3 * (size_t)i] = R.N[3 * (size_t)i + 1] = R.N[3 * (size_t)i + 2] = 0.0f;
   }
+}
+
+// traceRay(o, d, 0) (FULL, max_depth 2) for a list of rays (rt_trace_color): colour, first-hit face and t
+template <int TRAV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU)))
+void k_rays_color(FrameParams P, RayParams R) {
+  __shared__ WaveLds<TRAV, false> lds;
+  const int lane = threadIdx.x & 63, wv = (int)uniform(threadIdx.x >> 6);
+  const int base = (int)uniform((blockIdx.x * 4 + (threadIdx.x >> 6)) * 64);
+  if (base >= R.n) return;
+  const int i = base + lane;
+  const bool active = i < R.n;
+  const int j = active ? i : base;
+  Ray r;
+  r.o = ld3(R.o + 3 * (size_t)j);
+  r.d = ld3(R.d + 3 * (size_t)j);
+  r.o2 = affv3(P.Minv, r.o);
+  r.d2 = normalized(m3v3(P.MS, r.d));
+  setup_cull(r);
+  Hit h;
+  uint32_t face0;
+  const f3 col = trace_full<false, TRAV>(P, r, active, lds, wv, nullptr, h, face0);
+  if (!active) return;
+  R.rgb[3 * (size_t)i + 0] = col.x;
+  R.rgb[3 * (size_t)i + 1] = col.y;
+  R.rgb[3 * (size_t)i + 2] = col.z;
+  if (R.face) R.face[i] = face0 != 0xFFFFFFFFu ? (int32_t)face0 : -1;
+  if (R.t) R.t[i] = h.t;
 }
 
 // Output path: the float frame -> the PPM's 8-bit values on the device, so the host
@@ -1774,63 +1825,109 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* ligh
   return RT_OK;
 }
 
-static int trace_rays(rt_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t, float* P3,
-                      int32_t* blocked, bool any) {
+// ray-list queries: closest (face, t, P, optional interpolated normal), any-hit (blocked) or colour
+enum { Q_CLOSEST = 0, Q_SHADOW = 1, Q_COLOR = 2 };
+static int trace_rays(rt_scene* s, int query, int32_t n, const float* o, const float* d, int32_t* face, float* t,
+                      float* P3, float* N3, int32_t* blocked, float* rgb, const rt_light* lights, int32_t n_lights) {
   int rc = check_device_scene(s);
   if (rc) return rc;
-  if (n < 0 || (n && (!o || !d))) { set_error("trace: invalid arguments"); return RT_ERR_INVALID; }
+  if (n < 0 || (n && (!o || !d)) || n_lights < 0 || n_lights > RT_MAX_LIGHTS || (n_lights && !lights)) {
+    set_error("trace: invalid arguments");
+    return RT_ERR_INVALID;
+  }
   if (n == 0) return RT_OK;
   FrameParams P;
   fill_scene_params(s, P);
-  float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr, *d_P = nullptr;
-  int32_t *d_face = nullptr, *d_bl = nullptr;
+  if (query == Q_COLOR) {  // calculateColor's order: point lights, then directional lights
+    int k = 0;
+    for (int pass = 0; pass < 2; pass++)
+      for (int l = 0; l < n_lights; l++) {
+        const int kind = lights[l].kind == RT_LIGHT_DIRECTIONAL ? RT_LIGHT_DIRECTIONAL : RT_LIGHT_POINT;
+        if (kind != (pass ? RT_LIGHT_DIRECTIONAL : RT_LIGHT_POINT)) continue;
+        memcpy(P.lights[k].p, lights[l].position, 12);
+        memcpy(P.lights[k].c, lights[l].color, 12);
+        P.lights[k].kind = kind;
+        k++;
+      }
+    P.n_lights = n_lights;
+  }
   const size_t n3 = (size_t)n * 12;
   hipStream_t st = (hipStream_t)s->stream;
-  HIPCHECK(hipMalloc((void**)&d_o, n3));
-  HIPCHECK(hipMalloc((void**)&d_d, n3));
+  std::vector<void*> bufs;
+  struct Free {
+    std::vector<void*>& b;
+    ~Free() { for (void* p : b) (void)hipFree(p); }
+  } free_{bufs};
+  auto dalloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    bufs.push_back(p);
+    return p;
+  };
+  RayParams R{};
+  R.n = n;
+  float* d_o = (float*)dalloc(n3);
+  float* d_d = (float*)dalloc(n3);
+  if (!d_o || !d_d) { set_error("trace: device allocation failed"); return RT_ERR_NOMEM; }
   HIPCHECK(hipMemcpy(d_o, o, n3, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(d_d, d, n3, hipMemcpyHostToDevice));
-  RayParams R{d_o, d_d, n, nullptr, nullptr, nullptr, nullptr};
-  if (any) {
-    HIPCHECK(hipMalloc((void**)&d_bl, (size_t)n * 4));
-    R.blocked = d_bl;
+  R.o = d_o;
+  R.d = d_d;
+  if (query == Q_SHADOW) {
+    if (!(R.blocked = (int32_t*)dalloc((size_t)n * 4))) { set_error("trace: device allocation failed"); return RT_ERR_NOMEM; }
   } else {
-    HIPCHECK(hipMalloc((void**)&d_face, (size_t)n * 4));
-    HIPCHECK(hipMalloc((void**)&d_t, (size_t)n * 4));
-    R.face = d_face;
-    R.t = d_t;
-    if (P3) { HIPCHECK(hipMalloc((void**)&d_P, n3)); R.P = d_P; }
+    R.face = (int32_t*)dalloc((size_t)n * 4);
+    R.t = (float*)dalloc((size_t)n * 4);
+    if (!R.face || !R.t) { set_error("trace: device allocation failed"); return RT_ERR_NOMEM; }
+    if (query == Q_CLOSEST && P3 && !(R.P = (float*)dalloc(n3))) { set_error("trace: device allocation failed"); return RT_ERR_NOMEM; }
+    if (query == Q_CLOSEST && N3 && !(R.N = (float*)dalloc(n3))) { set_error("trace: device allocation failed"); return RT_ERR_NOMEM; }
+    if (query == Q_COLOR && !(R.rgb = (float*)dalloc(n3))) { set_error("trace: device allocation failed"); return RT_ERR_NOMEM; }
   }
   const int grid = (n + 255) / 256;
-  if (pick_trav(P, kernel_variant()) == TRAV_W4) {
-    if (any) hipLaunchKernelGGL((k_rays<true, TRAV_W4>), dim3(grid), dim3(256), 0, st, P, R);
+  const bool w4 = pick_trav(P, kernel_variant()) == TRAV_W4;
+  if (query == Q_COLOR) {
+    if (w4) hipLaunchKernelGGL((k_rays_color<TRAV_W4>), dim3(grid), dim3(256), 0, st, P, R);
+    else hipLaunchKernelGGL((k_rays_color<TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P, R);
+  } else if (w4) {
+    if (query == Q_SHADOW) hipLaunchKernelGGL((k_rays<true, TRAV_W4>), dim3(grid), dim3(256), 0, st, P, R);
     else hipLaunchKernelGGL((k_rays<false, TRAV_W4>), dim3(grid), dim3(256), 0, st, P, R);
   } else {
-    if (any) hipLaunchKernelGGL((k_rays<true, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P, R);
+    if (query == Q_SHADOW) hipLaunchKernelGGL((k_rays<true, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P, R);
     else hipLaunchKernelGGL((k_rays<false, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P, R);
   }
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(st));
-  if (any) {
-    HIPCHECK(hipMemcpy(blocked, d_bl, (size_t)n * 4, hipMemcpyDeviceToHost));
+  if (query == Q_SHADOW) {
+    HIPCHECK(hipMemcpy(blocked, R.blocked, (size_t)n * 4, hipMemcpyDeviceToHost));
   } else {
-    if (face) HIPCHECK(hipMemcpy(face, d_face, (size_t)n * 4, hipMemcpyDeviceToHost));
-    if (t) HIPCHECK(hipMemcpy(t, d_t, (size_t)n * 4, hipMemcpyDeviceToHost));
-    if (P3) HIPCHECK(hipMemcpy(P3, d_P, n3, hipMemcpyDeviceToHost));
+    if (face) HIPCHECK(hipMemcpy(face, R.face, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (t) HIPCHECK(hipMemcpy(t, R.t, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (R.P) HIPCHECK(hipMemcpy(P3, R.P, n3, hipMemcpyDeviceToHost));
+    if (R.N) HIPCHECK(hipMemcpy(N3, R.N, n3, hipMemcpyDeviceToHost));
+    if (R.rgb) HIPCHECK(hipMemcpy(rgb, R.rgb, n3, hipMemcpyDeviceToHost));
   }
-  for (void* b : {(void*)d_o, (void*)d_d, (void*)d_t, (void*)d_P, (void*)d_face, (void*)d_bl})
-    if (b) (void)hipFree(b);
   return RT_OK;
 }
 
 extern "C" int rt_trace_closest(rt_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t,
                                 float* P3) {
-  return trace_rays(s, n, o, d, face, t, P3, nullptr, false);
+  return trace_rays(s, Q_CLOSEST, n, o, d, face, t, P3, nullptr, nullptr, nullptr, nullptr, 0);
+}
+
+extern "C" int rt_trace_closest_normal(rt_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t,
+                                       float* P3, float* N3) {
+  return trace_rays(s, Q_CLOSEST, n, o, d, face, t, P3, N3, nullptr, nullptr, nullptr, 0);
 }
 
 extern "C" int rt_trace_shadow(rt_scene* s, int32_t n, const float* P3, const float* L3, int32_t* blocked) {
   if (!blocked && n > 0) { set_error("rt_trace_shadow: null output"); return RT_ERR_INVALID; }
-  return trace_rays(s, n, P3, L3, nullptr, nullptr, nullptr, blocked, true);
+  return trace_rays(s, Q_SHADOW, n, P3, L3, nullptr, nullptr, nullptr, nullptr, blocked, nullptr, nullptr, 0);
+}
+
+extern "C" int rt_trace_color(rt_scene* s, int32_t n, const float* o, const float* d, const rt_light* lights,
+                              int32_t n_lights, float* rgb, int32_t* face, float* t) {
+  if (!rgb && n > 0) { set_error("rt_trace_color: null output"); return RT_ERR_INVALID; }
+  return trace_rays(s, Q_COLOR, n, o, d, face, t, nullptr, nullptr, nullptr, rgb, lights, n_lights);
 }
 
 extern "C" int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out) {

@@ -456,9 +456,8 @@ extern "C" int32_t rt_lights_spherical(const rt_light* centre, float radius, int
   return n_points + 1;
 }
 
-extern "C" void rt_light_directional(const rt_camera* c, const float color[3], rt_light* out) {
-  // screenToWorld(Vector2f(viewport(2) / 2, viewport(3) / 2)) (camera.hpp:155-173), the point itself
-  const float px = c->viewport[2] / 2, py = c->viewport[3] / 2;
+// Camera::screenToWorld (camera.hpp:155-173) of a (float) screen position
+static f3 screen_to_world(const rt_camera* c, float px, float py) {
   f3 nc;
   nc.x = (float)(2.0 * (double)(px - c->viewport[0]) / (double)c->viewport[2] - 1.0);
   nc.y = (float)(1.0 - 2.0 * (double)(py - c->viewport[1]) / (double)c->viewport[3]);
@@ -469,10 +468,60 @@ extern "C" void rt_light_directional(const rt_camera* c, const float color[3], r
   nc.y = nc.y * scale;
   float vinv[16];
   rt::affinv(c->view_matrix, vinv);
-  const f3 w = rt::affv3(vinv, nc);
+  return rt::affv3(vinv, nc);
+}
+
+// Camera::getCenter (camera.hpp:115-118): view.linear().inverse() * (-view.translation())
+static f3 camera_center(const rt_camera* c) {
+  float L[9], Li[9];
+  rt::linear_of(c->view_matrix, L);
+  rt::m3inv(L, Li);
+  return rt::m3v3(Li, f3{-c->view_matrix[12], -c->view_matrix[13], -c->view_matrix[14]});
+}
+
+extern "C" void rt_light_directional(const rt_camera* c, const float color[3], rt_light* out) {
+  // screenToWorld(Vector2f(viewport(2) / 2, viewport(3) / 2)): the point itself is stored
+  const f3 w = screen_to_world(c, c->viewport[2] / 2, c->viewport[3] / 2);
   out->position[0] = w.x; out->position[1] = w.y; out->position[2] = w.z;
   for (int k = 0; k < 3; k++) out->color[k] = color[k];
   out->kind = RT_LIGHT_DIRECTIONAL;
+}
+
+// createDebugRay (flyscene.cpp:129-173) without the GL cylinders: the camera ray through the mouse
+// position, its traceRay colour, and the chain of reflections. As the reference, every segment gets the
+// first ray's colour, each reflection reflects the *first* direction about the new hit's interpolated
+// normal, and a miss ends the chain with a 10-unit segment. All ray queries run on the device.
+extern "C" int rt_debug_ray(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights, float mouse_x,
+                            float mouse_y, int32_t max_depth, rt_ray_segment* out, int32_t* n_out) {
+  if (!s || !cam || !out || !n_out || max_depth < 1) { rt::set_error("rt_debug_ray: invalid arguments"); return RT_ERR_INVALID; }
+  *n_out = 0;
+  const f3 origin = camera_center(cam);
+  const f3 dir = rt::normalized(rt::sub(screen_to_world(cam, mouse_x, mouse_y), origin));
+  float o[3] = {origin.x, origin.y, origin.z}, d[3] = {dir.x, dir.y, dir.z}, rgb[3];
+  int rc = rt_trace_color(s, 1, o, d, lights, n_lights, rgb, nullptr, nullptr);
+  if (rc) return rc;
+  for (int32_t i = 1; i <= max_depth; i++) {
+    int32_t face;
+    float t, P[3], N[3];
+    if ((rc = rt_trace_closest_normal(s, 1, o, d, &face, &t, P, N))) return rc;
+    rt_ray_segment& g = out[i - 1];
+    memcpy(g.origin, o, 12);
+    memcpy(g.direction, d, 12);
+    memcpy(g.color, rgb, 12);
+    *n_out = i;
+    if (t == INFINITY) {
+      g.length = 10.0f;
+      return RT_OK;
+    }
+    g.length = t;
+    if (i != max_depth) {
+      const f3 dn = rt::reflect(dir, f3{N[0], N[1], N[2]});
+      const f3 start = rt::offset(f3{P[0], P[1], P[2]}, dn, 0.001f);
+      o[0] = start.x; o[1] = start.y; o[2] = start.z;
+      d[0] = dn.x; d[1] = dn.y; d[2] = dn.z;
+    }
+  }
+  return RT_OK;
 }
 
 extern "C" void rt_camera_flycam(int32_t W, int32_t H, float dx, float dy, float dz, rt_camera* c) {

@@ -164,6 +164,8 @@ struct RayParams {
   float* t;
   float* P;
   int32_t* blocked;
+  float* N;        // [n][3] interpolated normal at the closest hit (optional)
+  float* rgb;      // [n][3] traceRay colour (rt_trace_color)
 };
 
 }  // namespace rt

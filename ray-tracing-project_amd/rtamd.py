@@ -28,6 +28,7 @@ EXPORTS = [
     "rt_debug_set_variant", "rt_scene_save", "rt_scene_load",
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
+    "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray",
 ]
 
 
@@ -60,6 +61,11 @@ class SceneInfo(C.Structure):
 class Camera(C.Structure):
     _fields_ = [("view_matrix", C.c_float * 16), ("viewport", C.c_float * 4), ("fovy", C.c_float),
                 ("aspect_ratio", C.c_float)]
+
+
+class RaySegment(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("direction", C.c_float * 3), ("length", C.c_float),
+                ("color", C.c_float * 3)]
 
 
 class Light(C.Structure):
@@ -129,6 +135,10 @@ def lib():
         L.rt_frame_download_rgb8.argtypes = [vp, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
         L.rt_frame_shard_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+        L.rt_trace_closest_normal.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, vp]
+        L.rt_trace_color.argtypes = [vp, C.c_int32, vp, vp, vp, C.c_int32, vp, vp, vp]
+        L.rt_debug_ray.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.c_float, C.c_float, C.c_int32, vp,
+                                   C.POINTER(C.c_int32)]
         L.rt_rand_seed.argtypes = [C.POINTER(RandState), C.c_uint32]
         L.rt_rand_seed.restype = None
         L.rt_rand.argtypes = [C.POINTER(RandState)]
@@ -265,6 +275,39 @@ class Scene:
         ex = C.c_int32(0)
         check(lib().rt_frame_download_rgb8(self.h, _p(out), C.byref(ex)))
         return out, bool(ex.value)
+
+    def trace_color(self, o, d, lights):
+        """traceRay colour (FULL) of arbitrary rays: rgb [n,3], face [n], t [n]"""
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        n = len(o)
+        rgb = np.zeros((n, 3), np.float32)
+        face = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        L = self._lights(lights)
+        check(lib().rt_trace_color(self.h, n, _p(o), _p(d), C.cast(L, C.c_void_p), len(lights), _p(rgb), _p(face), _p(t)))
+        return rgb, face, t
+
+    def trace_closest_normal(self, o, d):
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        n = len(o)
+        face = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        P = np.zeros((n, 3), np.float32)
+        N = np.zeros((n, 3), np.float32)
+        check(lib().rt_trace_closest_normal(self.h, n, _p(o), _p(d), _p(face), _p(t), _p(P), _p(N)))
+        return face, t, P, N
+
+    def debug_ray(self, cam, lights, mouse_x, mouse_y, max_depth=2):
+        """createDebugRay: [(origin3, direction3, length, color3), ...]"""
+        segs = (RaySegment * max_depth)()
+        n = C.c_int32(0)
+        L = self._lights(lights)
+        check(lib().rt_debug_ray(self.h, C.byref(cam), C.cast(L, C.c_void_p), len(lights), mouse_x, mouse_y, max_depth,
+                                 segs, C.byref(n)))
+        return [(np.array(g.origin, np.float32), np.array(g.direction, np.float32), np.float32(g.length),
+                 np.array(g.color, np.float32)) for g in segs[: n.value]]
 
     def pack_shard_rgb8(self, dst_device_ptr):
         """This rank's tiles of the last frame, 8-bit, into device memory (rt_frame_pack_shard_rgb8)."""

@@ -338,3 +338,34 @@ def test_gpu_lbvh_builder(rt, soup, name):
         b = lb.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
         for x, y in zip(a[:3], b[:3]):
             assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (name, m)
+
+
+def test_trace_color_and_debug_ray(rt, orc):
+    """f4 single-ray queries: traceRay colours of camera rays equal the FULL frame's pixels bit for bit;
+    the debug ray's first segment is that pixel's ray, colour and hit distance, and each reflection
+    segment starts 0.001 along its direction from the previous hit."""
+    W, H = 480, 270
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    cam = rt.flycam(W, H, 0, 0, 20)
+    rgb, face, t, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_FULL, want_hits=True)
+    ocam = orc.flycam(W, H, 0, 0, 20)
+    pix = [(i, j) for j in range(3, H, 17) for i in range(5, W, 23)]
+    od = [orc.camera_ray(ocam, i, j) for i, j in pix]
+    o = np.array([a for a, _ in od], np.float32)
+    d = np.array([b for _, b in od], np.float32)
+    c, f, tt = sc.trace_color(o, d, rt.DEFAULT_LIGHTS)
+    ii = np.array([p[0] for p in pix]); jj = np.array([p[1] for p in pix])
+    assert c.tobytes() == rgb[jj, ii].tobytes()
+    assert (f == face[jj, ii]).all() and tt.tobytes() == t[jj, ii].tobytes()
+    hits = [(i, j) for i, j in pix if face[j, i] >= 0][:20]
+    assert hits
+    for i, j in hits:
+        segs = sc.debug_ray(cam, rt.DEFAULT_LIGHTS, float(i), float(j), max_depth=3)
+        o0, d0 = orc.camera_ray(ocam, i, j)
+        assert segs[0][0].tobytes() == np.asarray(o0, np.float32).tobytes()
+        assert segs[0][1].tobytes() == np.asarray(d0, np.float32).tobytes()
+        assert segs[0][2] == t[j, i] and segs[0][3].tobytes() == rgb[j, i].tobytes()
+        for a, b in zip(segs, segs[1:]):
+            hitp = a[0] + a[2] * a[1]
+            assert np.allclose(b[0], hitp + np.float32(0.001) * b[1], atol=1e-5)
+            assert (b[3] == segs[0][3]).all()
