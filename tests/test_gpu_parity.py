@@ -369,3 +369,19 @@ def test_trace_color_and_debug_ray(rt, orc):
             hitp = a[0] + a[2] * a[1]
             assert np.allclose(b[0], hitp + np.float32(0.001) * b[1], atol=1e-5)
             assert (b[3] == segs[0][3]).all()
+
+
+def test_counting_frame_among_frames_in_flight(rt, soup):
+    """A counting (RT_FRAME_STATS) frame queued between ordinary frames in flight reports the same
+    counters as a counting frame rendered alone (the shared counters are not disturbed)."""
+    sc, _ = soup
+    W, H = 1920, 1080
+    cam = rt.flycam(W, H, 0, 0, 20)
+    sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS)
+    alone = sc.synchronize()
+    for k in range(3):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H)
+    sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS)
+    mixed = sc.synchronize()
+    for key in ("node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "hits", "total_rays"):
+        assert mixed[key] == alone[key], key
