@@ -47,17 +47,24 @@ void Flyscene::initialize(int width, int height, const std::string& obj_path, in
   flycamera.setPerspectiveMatrix(60.0f, width / (float)height);
   flycamera.setViewport((float)width, (float)height);
   flycamera.reset();
+  lights.push_back({Vec3{-0.5f, 2.0f, 3.0f}, Vec3{1.0f, 1.0f, 1.0f}});
+  rt_scene_opts o;
+  rt_scene_opts_default(&o);
+  o.device = device;
+  o.builder = builder;
+  // a scene cache skips OBJ parsing and every build
+  if (!cache_path.empty() && rt_scene_load(cache_path.c_str(), &o, &scene_) == RT_OK) return;
   if (rt_mesh_load_obj(obj_path.c_str(), &mesh_) != RT_OK) {
     fprintf(stderr, "%s\n", rt_last_error());  // reference: "Cannot open", empty mesh
     return;
   }
-  lights.push_back({Vec3{-0.5f, 2.0f, 3.0f}, Vec3{1.0f, 1.0f, 1.0f}});
   rt_mesh_desc d;
   rt_mesh_get_desc(mesh_, &d);
-  rt_scene_opts o;
-  rt_scene_opts_default(&o);
-  o.device = device;
-  if (rt_scene_create(&d, &o, &scene_) != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
+  if (rt_scene_create(&d, &o, &scene_) != RT_OK) {
+    fprintf(stderr, "%s\n", rt_last_error());
+    return;
+  }
+  if (!cache_path.empty() && rt_scene_save(scene_, cache_path.c_str()) != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
 }
 
 double Flyscene::raytraceScene(int width, int height) {

@@ -60,6 +60,8 @@ class Flyscene {
   int mode = RT_MODE_FULL;               // the reference traceRay (max_depth 2, shadows)
   std::string output = "result.ppm";
   std::vector<float> last_image;         // [H][W][3] float frame (kept only when the 8-bit path was inexact)
+  std::string cache_path;                // binary scene cache: loaded if present, written after a build
+  int builder = RT_BUILDER_SAH;          // RT_BUILDER_LBVH_GPU: build the BVH on the GPU
 
  private:
   Flycamera flycamera;

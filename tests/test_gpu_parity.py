@@ -385,3 +385,25 @@ def test_counting_frame_among_frames_in_flight(rt, soup):
     mixed = sc.synchronize()
     for key in ("node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "hits", "total_rays"):
         assert mixed[key] == alone[key], key
+
+
+def test_cli_flyscene_mirror(rt, tmp_path):
+    """The Flyscene-shaped host (rt_render_cli: initialize -> translate -> raytraceScene -> result.ppm):
+    its PPM (8-bit download path) is byte-identical to writePPMImage of the library's float frame, also
+    when the scene comes from the binary cache or from the GPU LBVH build."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ray-tracing-project_amd", "lib",
+                       "rt_render_cli")
+    obj = scene_path("bunny.obj")
+    W, H = 320, 180
+    sc = rt.Scene(rt.Mesh.load_obj(obj))
+    rgb, _ = sc.render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_FULL)
+    ref = tmp_path / "ref.ppm"
+    rt.write_ppm(ref, rgb)
+    cache = tmp_path / "bunny.rtscene"
+    for extra in ([], ["--cache", str(cache)], ["--cache", str(cache)], ["--lbvh"]):
+        out = tmp_path / "out.ppm"
+        subprocess.check_call([cli, obj, str(W), str(H), "--dz", "20", "--out", str(out)] + extra,
+                              stdout=subprocess.DEVNULL)
+        assert out.read_bytes() == ref.read_bytes(), extra
+    assert cache.exists()
