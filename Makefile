@@ -28,20 +28,24 @@ $(OBJ)/rt_build.o: $(PKG)/csrc/rt_build.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-result -c $< -o $@
 
+$(OBJ)/rt_boxes.o: $(PKG)/csrc/rt_boxes.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(OBJ)/rt_cache.o: $(PKG)/csrc/rt_cache.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o
+$(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o
 	@mkdir -p $(PKG)/lib
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
 # A/B builds of the same sources with extra device flags (experiments only):
 #   make ablib TAG=noslp EXTRA="-fno-slp-vectorize"  ->  lib/librtamd_noslp.so  (select with RTAMD_LIB)
-ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o
+ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o
 	@mkdir -p $(OBJ) $(PKG)/lib
 	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $(OBJ)/rt_device_$(TAG).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o -lpthread
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o -lpthread
 
 cli: $(PKG)/lib/rt_render_cli
 

@@ -105,10 +105,16 @@ typedef struct rt_scene_opts {
   int32_t builder;          /* RT_BUILDER_SAH (host binned SAH, default: fastest traversal) or
                              * RT_BUILDER_LBVH_GPU (Morton/radix-sort/Karras build on the
                              * device in milliseconds; falls back to SAH when the tree would be too deep) */
+  int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_HOST (default,
+                             * parallel passes on the host) or RT_BOXES_GPU (one launch per pass,
+                             * one workgroup per box; identical boxes and face order; scenes with
+                             * non-finite vertex coordinates use the host builder) */
 } rt_scene_opts;
 
 #define RT_BUILDER_SAH 0
 #define RT_BUILDER_LBVH_GPU 1
+#define RT_BOXES_HOST 0
+#define RT_BOXES_GPU 1
 
 void rt_scene_opts_default(rt_scene_opts* o);
 
@@ -131,6 +137,8 @@ typedef struct rt_scene_info {
   double upload_ms;       /* the device upload */
   int32_t builder;        /* the builder actually used (RT_BUILDER_*) */
   double bvh_gpu_ms;      /* device time of the LBVH kernels (RT_BUILDER_LBVH_GPU) */
+  int32_t box_builder;    /* the box partition builder actually used (RT_BOXES_*) */
+  double boxes_gpu_ms;    /* device time of the GPU box partition (RT_BOXES_GPU) */
 } rt_scene_info;
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);

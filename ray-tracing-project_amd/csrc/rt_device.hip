@@ -185,7 +185,7 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  cand &= ~ballot((dot(n, a0) < 0) | (dot(n, a1) < 0) | (dot(n, a2) < 0));
+  cand &= ~ballot((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0));
   if (cand == 0) return;
   const bool acc = lane_in(accept_candidate(P, tr, e0, e2, a0, a1, a2, p, r, cand));
   if (ANY) {
@@ -471,7 +471,7 @@ __device__ __forceinline__ void test_tri_lane(const DevScene& P, const TriRec64&
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  if ((dot(n, a0) < 0) | (dot(n, a1) < 0) | (dot(n, a2) < 0)) return;
+  if ((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0)) return;
   if (!accept_lane(P, tr, e0, e2, a0, a1, a2, p, r)) return;
   if (ANY) {
     found = true;

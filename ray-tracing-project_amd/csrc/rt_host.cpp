@@ -685,6 +685,10 @@ void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t 
     for (size_t i = 0; i < todo.size(); i++)
       if (made[i]) hs.boxes.push_back(std::move(created[i]));
   }
+  assign_box_ranks(hs);
+}
+
+void assign_box_ranks(HostScene& hs) {
   hs.face_rank.assign(hs.nf, 0);
   hs.face_box.assign(hs.nf, 0);
   uint32_t rank = 0;
@@ -1239,8 +1243,27 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   s->prep_ms = ms_since(t0);
   auto t1 = clk::now();
-  rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
+  bool boxes_done = false;
+  if (s->opts.box_builder == RT_BOXES_GPU && s->opts.device != RT_DEVICE_NONE) {
+    int dev = s->opts.device;
+    if (dev < 0) dev = rt::current_device();
+    bool nonfinite = false;
+    if (dev >= 0) {
+      const int rc = rt::gpu_build_ref_boxes(dev, hs, d->vertices, s->opts.min_faces, s->opts.max_boxes,
+                                             &s->boxes_gpu_ms, &nonfinite);
+      if (rc) { delete s; return rc; }
+      if (!nonfinite) {
+        rt::assign_box_ranks(hs);
+        boxes_done = true;
+        s->box_builder_used = RT_BOXES_GPU;
+      }
+    }
+  }
+  if (!boxes_done) rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
   s->boxes_ms = ms_since(t1);
+  if (getenv("RT_TIMING"))
+    fprintf(stderr, "[rt] boxes %.1f ms (%s, device %.1f ms), %zu boxes\n", s->boxes_ms,
+            s->box_builder_used == RT_BOXES_GPU ? "gpu" : "host", s->boxes_gpu_ms, hs.boxes.size());
   auto t2 = clk::now();
   bool built = false;
   if (s->opts.builder == RT_BUILDER_LBVH_GPU && s->opts.device != RT_DEVICE_NONE) {
@@ -1298,6 +1321,8 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->upload_ms = s->upload_ms;
   o->builder = s->builder_used;
   o->bvh_gpu_ms = s->bvh_gpu_ms;
+  o->box_builder = s->box_builder_used;
+  o->boxes_gpu_ms = s->boxes_gpu_ms;
   return RT_OK;
 }
 

@@ -47,6 +47,12 @@ struct HostScene {
 };
 
 void build_ref_boxes(HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes);
+// the same partition on the GPU (rt_boxes.hip); *nonfinite: some vertex coordinate is not finite and
+// nothing was built (the caller uses the host builder)
+int gpu_build_ref_boxes(int device, HostScene& hs, const float* v4, int32_t min_faces, int32_t max_boxes,
+                        double* gpu_ms, bool* nonfinite);
+// face_rank / face_box from hs.boxes (boxes in creation order, faces in in-box order)
+void assign_box_ranks(HostScene& hs);
 void build_bvh(HostScene& hs, int leaf_size);
 bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
@@ -59,7 +65,8 @@ void set_error(const char* fmt, ...);
 struct rt_scene {
   rt_scene_opts opts;
   rt::HostScene hs;
-  double build_ms = 0.0, prep_ms = 0.0, boxes_ms = 0.0, bvh_ms = 0.0, upload_ms = 0.0, bvh_gpu_ms = 0.0;
+  double build_ms = 0.0, prep_ms = 0.0, boxes_ms = 0.0, bvh_ms = 0.0, upload_ms = 0.0, bvh_gpu_ms = 0.0, boxes_gpu_ms = 0.0;
+  int32_t box_builder_used = 0;
   int32_t builder_used = 0;
   int32_t device = RT_DEVICE_NONE;
   // device state (rt_device.hip)

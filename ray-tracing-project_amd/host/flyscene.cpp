@@ -52,6 +52,7 @@ void Flyscene::initialize(int width, int height, const std::string& obj_path, in
   rt_scene_opts_default(&o);
   o.device = device;
   o.builder = builder;
+  o.box_builder = box_builder;
   // a scene cache skips OBJ parsing and every build
   if (!cache_path.empty() && rt_scene_load(cache_path.c_str(), &o, &scene_) == RT_OK) return;
   if (rt_mesh_load_obj(obj_path.c_str(), &mesh_) != RT_OK) {

@@ -62,6 +62,7 @@ class Flyscene {
   std::vector<float> last_image;         // [H][W][3] float frame (kept only when the 8-bit path was inexact)
   std::string cache_path;                // binary scene cache: loaded if present, written after a build
   int builder = RT_BUILDER_SAH;          // RT_BUILDER_LBVH_GPU: build the BVH on the GPU
+  int box_builder = RT_BOXES_HOST;       // RT_BOXES_GPU: build the reference box partition on the GPU
 
  private:
   Flycamera flycamera;

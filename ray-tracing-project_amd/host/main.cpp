@@ -1,7 +1,7 @@
 // main.cpp -- headless stand-in for the reference's src/main.cpp key-'T' path (main.cpp:68-69):
 // initialize a Flyscene, optionally move the Flycamera, ray trace, write the PPM.
 //   rt_render_cli <scene.obj> [W H] [--primary] [--dz N] [--out result.ppm] [--device D] [--cache file]
-//                 [--lbvh]
+//                 [--lbvh] [--gpu-boxes]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -11,12 +11,12 @@
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    fprintf(stderr, "usage: %s scene.obj [W H] [--primary] [--dz N] [--out file.ppm] [--device D] [--cache file] [--lbvh]\n",
+    fprintf(stderr, "usage: %s scene.obj [W H] [--primary] [--dz N] [--out file.ppm] [--device D] [--cache file] [--lbvh] [--gpu-boxes]\n",
             argv[0]);
     return 2;
   }
   std::string obj = argv[1], out = "result.ppm", cache;
-  int builder = RT_BUILDER_SAH;
+  int builder = RT_BUILDER_SAH, box_builder = RT_BOXES_HOST;
   int W = 1000, H = 1000, device = -1, mode = RT_MODE_FULL;
   float dz = 0.0f;
   int pos = 0;
@@ -27,12 +27,14 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--cache") && i + 1 < argc) cache = argv[++i];
     else if (!strcmp(argv[i], "--lbvh")) builder = RT_BUILDER_LBVH_GPU;
+    else if (!strcmp(argv[i], "--gpu-boxes")) box_builder = RT_BOXES_GPU;
     else if (pos == 0) { W = atoi(argv[i]); pos++; }
     else if (pos == 1) { H = atoi(argv[i]); pos++; }
   }
   fly::Flyscene scene;
   scene.cache_path = cache;
   scene.builder = builder;
+  scene.box_builder = box_builder;
   scene.initialize(W, H, obj, device);
   scene.mode = mode;
   scene.output = out;

@@ -47,7 +47,7 @@ class MeshDesc(C.Structure):
 class SceneOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("min_faces", C.c_int32), ("max_boxes", C.c_int32),
                 ("leaf_size", C.c_int32), ("default_material", Material), ("background", C.c_float * 3),
-                ("frames_in_flight", C.c_int32), ("builder", C.c_int32)]
+                ("frames_in_flight", C.c_int32), ("builder", C.c_int32), ("box_builder", C.c_int32)]
 
 
 class SceneInfo(C.Structure):
@@ -55,7 +55,8 @@ class SceneInfo(C.Structure):
                 ("bvh_nodes", C.c_int32), ("bvh_leaves", C.c_int32), ("bvh_depth", C.c_int32),
                 ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("device", C.c_int32),
                 ("prep_ms", C.c_double), ("boxes_ms", C.c_double), ("bvh_ms", C.c_double), ("upload_ms", C.c_double),
-                ("builder", C.c_int32), ("bvh_gpu_ms", C.c_double)]
+                ("builder", C.c_int32), ("bvh_gpu_ms", C.c_double), ("box_builder", C.c_int32),
+                ("boxes_gpu_ms", C.c_double)]
 
 
 class Camera(C.Structure):
@@ -240,12 +241,15 @@ class Mesh:
 
 
 RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU = 0, 1
+RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 
-def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=0):
+def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=0,
+               box_builder=0):
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
     o.builder = builder
+    o.box_builder = box_builder
     if background is not None:
         o.background[:] = [float(x) for x in background]
     o.device = device
@@ -257,11 +261,12 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, backgr
 
 
 class Scene:
-    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=0):
+    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=0,
+                 box_builder=0):
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
         self.h = C.c_void_p()
         d = mesh.desc()
-        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder)
+        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder, box_builder)
         check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
 
     def info(self):

@@ -401,9 +401,71 @@ def test_cli_flyscene_mirror(rt, tmp_path):
     ref = tmp_path / "ref.ppm"
     rt.write_ppm(ref, rgb)
     cache = tmp_path / "bunny.rtscene"
-    for extra in ([], ["--cache", str(cache)], ["--cache", str(cache)], ["--lbvh"]):
+    for extra in ([], ["--cache", str(cache)], ["--cache", str(cache)], ["--lbvh", "--gpu-boxes"]):
         out = tmp_path / "out.ppm"
         subprocess.check_call([cli, obj, str(W), str(H), "--dz", "20", "--out", str(out)] + extra,
                               stdout=subprocess.DEVNULL)
         assert out.read_bytes() == ref.read_bytes(), extra
     assert cache.exists()
+
+
+def _tie_mesh(rt, n, seed):
+    """Faces whose coordinates come from a tiny set incl. -0.0 / +0.0: ties in every min / max, many
+    impossible split axes (axis retries) and duplicate faces."""
+    rng = np.random.default_rng(seed)
+    vals = np.array([-1.0, -0.0, 0.0, 0.25, 1.0], np.float32)
+    v = vals[rng.integers(0, len(vals), size=(3 * n, 3))]
+    f = np.arange(3 * n, dtype=np.uint32).reshape(-1, 3)
+    return rt.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32))
+
+
+def _box_case(rt, soup, name):
+    if name == "soup":
+        return soup[0].mesh, 300
+    if name == "ties":
+        return _tie_mesh(rt, 20000, 7), 20
+    if name == "same":  # every face identical: all three axes fail, one box
+        v = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (400, 1))
+        f = np.arange(1200, dtype=np.uint32).reshape(-1, 3)
+        return rt.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32)), 300
+    scene, mf = name.split(":")
+    return rt.Mesh.load_obj(scene_path(scene + ".obj")), int(mf)
+
+
+@pytest.mark.parametrize("name", ["cube:300", "dodgeColorTest:300", "bunny:300", "bunny:8", "testding:40", "soup",
+                                  "ties", "same"])
+def test_gpu_box_partition(rt, soup, name):
+    """f2: generateBoundingBoxes on the device -- the same boxes (bounds bit for bit), the same box order
+    and the same in-box face order as the host restatement (itself pinned to the oracle and the survey's
+    reference box counts), hence the same tie-break ranks."""
+    mesh, mf = _box_case(rt, soup, name)
+    host = rt.Scene(mesh, min_faces=mf)
+    dev = rt.Scene(mesh, min_faces=mf, box_builder=rt.RT_BOXES_GPU)
+    ih, idv = host.info(), dev.info()
+    assert ih["box_builder"] == rt.RT_BOXES_HOST and idv["box_builder"] == rt.RT_BOXES_GPU
+    assert idv["boxes_gpu_ms"] > 0
+    hb, db = host.ref_boxes(), dev.ref_boxes()
+    assert ih["n_ref_boxes"] == idv["n_ref_boxes"], (ih["n_ref_boxes"], idv["n_ref_boxes"])
+    for a, b in zip(hb, db):
+        assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), name
+    if name == "same":
+        assert idv["n_ref_boxes"] == 1
+    if name in ("bunny:300", "ties"):
+        W, H = 480, 270
+        cam = rt.flycam(W, H, 0, 0, 20)
+        a = host.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_FULL, want_hits=True)
+        b = dev.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_FULL, want_hits=True)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes()
+
+
+def test_gpu_box_partition_nonfinite_uses_host(rt):
+    """A referenced vertex with a non-finite coordinate: the device builder declines, the host one runs."""
+    v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [np.nan, 0, 1], [1, 1, 1], [0, 1, 1]], np.float32)
+    f = np.arange(6, dtype=np.uint32).reshape(-1, 3)
+    mesh = rt.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32))
+    try:
+        sc = rt.Scene(mesh, box_builder=rt.RT_BOXES_GPU)
+    except rt.RTError:
+        return  # rejected later in scene creation: nothing built on the device either
+    assert sc.info()["box_builder"] == rt.RT_BOXES_HOST
