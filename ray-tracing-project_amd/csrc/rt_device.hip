@@ -104,6 +104,24 @@ __device__ __forceinline__ Span slab(float lx, float hx, float ly, float hy, flo
   s.tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_ray));
   return s;
 }
+// The same span when the wave's active rays share one direction octant (OCT bit k: axis k negative,
+// by the sign of the nudged reciprocal): fma(., id, oid) is monotone in the box coordinate, so the
+// near / far plane of each axis is known and min(t0, t1) / max(t0, t1) are exactly the near / far
+// values -- identical results with 8 fewer min/max per child. OCT < 0: the generic test.
+template <int OCT>
+__device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
+                                       float tmax_ray) {
+  if (OCT < 0) return slab(lx, hx, ly, hy, lz, hz, r, tmax_ray);
+  const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
+  const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
+  const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
+  Span s;
+  s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, r.oid.x), __builtin_fmaf(ny, r.id.y, r.oid.y)),
+                 fmaxf(__builtin_fmaf(nz, r.id.z, r.oid.z), 0.0f));
+  s.tmax = fminf(fminf(__builtin_fmaf(fx, r.id.x, r.oid.x), __builtin_fmaf(fy, r.id.y, r.oid.y)),
+                 fminf(__builtin_fmaf(fz, r.id.z, r.oid.z), tmax_ray));
+  return s;
+}
 // lane masks straight from v_cmp (no bool materialisation): llvm.amdgcn.fcmp predicates
 constexpr int kFcmpOLE = 5;
 __device__ __forceinline__ uint64_t mask_le(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOLE); }
@@ -206,7 +224,7 @@ struct WaveStack {
   int sp = 0;
 };
 
-template <bool ANY, bool STATS, bool STACK_LDS>
+template <bool ANY, bool STATS, bool STACK_LDS, int OCT = -1>
 __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                          uint32_t* lds_stack, uint32_t* cnt) {
   if (P.n_nodes == 0) return;
@@ -228,8 +246,8 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
         cnt[ST_WNODE]++;
       }
       const float tcut = ANY ? tmax_any : h.t;
-      const Span s0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
-      const Span s1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+      const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
+      const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
 #ifdef RT_EXPERIMENT_NODES_TWICE  // timing experiment only: the box tests once more on opaque copies
       {
         Ray r2 = r;
@@ -249,7 +267,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       const uint32_t far = first0 ? nd.child1 : nd.child0;
       // the far child is written above the top unconditionally and kept only when both are needed
       if (STACK_LDS) lds_stack[sp] = far;
-      else stackv = (lane_id() == sp) ? far : stackv;  // v_cmp + v_cndmask
+      else asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(stackv) : "s"(far), "s"(sp) : "m0");
       if (STATS) {
         const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
         const bool wf = first0 ? h1 : h0;
@@ -548,6 +566,37 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
   else traverse<ANY, STATS, TRAV == TRAV_B2_LDS>(P, r, active, h, found, L.stack[wv], cnt);
 }
 
+// Closest-hit packet traversal specialised by the wave's direction octant when every active ray shares
+// it (coherent camera / reflection packets); mixed-octant waves take the generic loop.
+#ifndef RT_OCT_SPECIALIZE
+#define RT_OCT_SPECIALIZE 1
+#endif
+template <bool STATS, int TRAV>
+__device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& r, bool active, Hit& h,
+                                                  WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
+  bool found = false;
+  if (RT_OCT_SPECIALIZE && (TRAV == TRAV_B2_LDS || TRAV == TRAV_B2_VGPR)) {
+    constexpr bool SL = TRAV == TRAV_B2_LDS;
+    const uint64_t act = ballot(active);
+    const uint64_t sx = ballot(__float_as_uint(r.id.x) >> 31) & act, sy = ballot(__float_as_uint(r.id.y) >> 31) & act,
+                   sz = ballot(__float_as_uint(r.id.z) >> 31) & act;
+    if ((sx == 0 || sx == act) && (sy == 0 || sy == act) && (sz == 0 || sz == act)) {
+      const int oct = (sx ? 1 : 0) | (sy ? 2 : 0) | (sz ? 4 : 0);
+      switch (oct) {
+        case 0: traverse<false, STATS, SL, 0>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 1: traverse<false, STATS, SL, 1>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 2: traverse<false, STATS, SL, 2>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 3: traverse<false, STATS, SL, 3>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 4: traverse<false, STATS, SL, 4>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 5: traverse<false, STATS, SL, 5>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 6: traverse<false, STATS, SL, 6>(P, r, active, h, found, L.stack[wv], cnt); return;
+        default: traverse<false, STATS, SL, 7>(P, r, active, h, found, L.stack[wv], cnt); return;
+      }
+    }
+  }
+  trace<false, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Shading
 // ------------------------------------------------------------------------------------------------
@@ -729,8 +778,7 @@ void k_trace_primary(FrameParams P) {
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && c.active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  bool dummy = false;
-  trace<false, STATS, TRAV>(P.sc, r, c.active, h, dummy, lds, c.slot, cnt);
+  trace_closest_oct<STATS, TRAV>(P.sc, r, c.active, h, lds, c.slot, cnt);
   if (STATS && c.active && h.t != INFINITY) cnt[ST_HITS]++;
   if (c.active) P.hits[(size_t)c.py * P.W + c.px] = make_uint2(__float_as_uint(h.t), h.slot);
   if (P.wcount0 != nullptr) {  // FULL pipeline: per-wave hit count for the list0 compaction
@@ -738,6 +786,72 @@ void k_trace_primary(FrameParams P) {
     if (c.lane == 0) P.wcount0[c.qw] = nh;
   }
   if (STATS) flush_stats(P, cnt, c.lane);
+}
+
+// Two rays per lane (128-ray packets, one 16x8 pixel half-tile per wave): the per-node scalar work
+// (fetch, decision, stack) is shared by twice as many rays and each lane carries two independent
+// slab / triangle streams. Closest hit only (PRIMARY), LDS stack.
+__device__ __forceinline__ void traverse_x2(const DevScene& P, const Ray& ra, const Ray& rb, bool acta, bool actb,
+                                            Hit& ha, Hit& hb, uint32_t* lds_stack) {
+  if (P.n_nodes == 0) return;
+  int sp = 0;
+  uint32_t node = P.root;
+  const uint64_t ma = ballot(acta), mb = ballot(actb);
+  bool dummy = false;
+  for (;;) {
+    bool pop = true;
+    if (!is_leaf(node)) {
+      const Node64 nd = sload_node(P.nodes, node);
+      const Span a0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, ra, ha.t);
+      const Span a1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, ra, ha.t);
+      const Span b0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, rb, hb.t);
+      const Span b1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, rb, hb.t);
+      const uint64_t m0a = mask_le(a0.tmin, a0.tmax) & ma, m1a = mask_le(a1.tmin, a1.tmax) & ma;
+      const uint64_t m0b = mask_le(b0.tmin, b0.tmax) & mb, m1b = mask_le(b1.tmin, b1.tmax) & mb;
+      const uint64_t v0a = m0a & (~m1a | mask_le(a0.tmin, a1.tmin));
+      const uint64_t v0b = m0b & (~m1b | mask_le(b0.tmin, b1.tmin));
+      const uint64_t M0 = m0a | m0b, M1 = m1a | m1b;
+      const bool first0 = 2 * (__popcll(v0a) + __popcll(v0b)) >= __popcll(m0a | m1a) + __popcll(m0b | m1b);
+      lds_stack[sp] = first0 ? nd.child1 : nd.child0;
+      sp += ((M0 != 0) & (M1 != 0)) ? 1 : 0;
+      node = first0 ? nd.child0 : nd.child1;
+      pop = (M0 | M1) == 0;
+    } else {
+      const uint32_t first = leaf_first(node), count = leaf_count(node);
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = sload_tri(P.tris, first + k);
+        test_tri<false>(P, tr, first + k, ra, ma, ha, dummy);
+        test_tri<false>(P, tr, first + k, rb, mb, hb, dummy);
+      }
+    }
+    if (pop) {
+      if (sp == 0) break;
+      sp--;
+      node = uniform(lds_stack[sp]);
+    }
+  }
+}
+
+#ifndef RT_X2_WAVES_PER_EU
+#define RT_X2_WAVES_PER_EU 6
+#endif
+// one 64-thread block per 16x8 half of a 16x16 tile (blocks 2t, 2t+1 cover tile t); lane (x, y) traces
+// pixels (x, y) and (x + 8, y) of its half
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_X2_WAVES_PER_EU)))
+void k_trace_primary_x2(FrameParams P) {
+  __shared__ uint32_t stack[64];
+  const int lane = threadIdx.x & 63;
+  const int nb = (int)(gridDim.x >> 1), b = (int)(blockIdx.x >> 1), half = (int)(blockIdx.x & 1);
+  (void)nb;
+  const int tile = P.shard_index + b * P.shard_count;
+  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  const int pxa = tx * 16 + (lane & 7), pxb = pxa + 8, py = ty * 16 + half * 8 + (lane >> 3);
+  const bool acta = pxa < P.W && py < P.H, actb = pxb < P.W && py < P.H;
+  const Ray ra = primary_ray(P, pxa, py), rb = primary_ray(P, pxb, py);
+  Hit ha{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu}, hb{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  traverse_x2(P.sc, ra, rb, acta, actb, ha, hb, stack);
+  if (acta) P.hits[(size_t)py * P.W + pxa] = make_uint2(__float_as_uint(ha.t), ha.slot);
+  if (actb) P.hits[(size_t)py * P.W + pxb] = make_uint2(__float_as_uint(hb.t), hb.slot);
 }
 
 // PRIMARY stage 2: traceRay at depth limit 1 without shadows: calculateColor (flyscene.cpp:603-614)
@@ -1639,7 +1753,10 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   HIPCHECK(hipEventRecord(ev_a, st));
   if (grid > 0) {
     if (fr->mode == RT_MODE_PRIMARY) {
-      if (stats) launch_trace<true>(P, grid, st, trav); else launch_trace<false>(P, grid, st, trav);
+      if (stats) launch_trace<true>(P, grid, st, trav);
+      else if ((variant & 256) && trav == TRAV_B2_LDS)
+        hipLaunchKernelGGL(k_trace_primary_x2, dim3(2 * grid), dim3(64), 0, st, P);
+      else launch_trace<false>(P, grid, st, trav);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));
       if (hits) hipLaunchKernelGGL(k_shade_primary<true>, dim3(grid), dim3(256), 0, st, P);

@@ -189,7 +189,7 @@ def test_stats_counting_run(rt, soup):
 
 
 VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "full-pipeline": 16, "pipeline-lane-refl": 48,
-            "pipeline-lane-all": 16 | 32 | 64 | 128}
+            "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256}
 
 
 @pytest.mark.parametrize("name", sorted(VARIANTS))
@@ -200,7 +200,7 @@ def test_kernel_variants_render_identical_bits(rt, soup, name):
     sc_soup, _ = soup
     bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
     cases = [(bunny, 1920, 1080, rt.RT_MODE_PRIMARY), (bunny, 1920, 1080, rt.RT_MODE_FULL),
-             (sc_soup, 640, 360, rt.RT_MODE_FULL)]
+             (sc_soup, 640, 360, rt.RT_MODE_FULL), (sc_soup, 1000, 563, rt.RT_MODE_PRIMARY)]
     for sc, W, H, m in cases:
         cam = rt.flycam(W, H, 0, 0, 20)
         prev = rt.set_variant(0)
