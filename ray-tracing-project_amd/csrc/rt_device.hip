@@ -108,6 +108,9 @@ __device__ __forceinline__ Span slab(float lx, float hx, float ly, float hy, flo
 // by the sign of the nudged reciprocal): fma(., id, oid) is monotone in the box coordinate, so the
 // near / far plane of each axis is known and min(t0, t1) / max(t0, t1) are exactly the near / far
 // values -- identical results with 8 fewer min/max per child. OCT < 0: the generic test.
+#ifndef RT_CLIP_ASM
+#define RT_CLIP_ASM 1
+#endif
 template <int OCT>
 __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
                                        float tmax_ray) {
@@ -118,8 +121,17 @@ __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, f
   Span s;
   s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, r.oid.x), __builtin_fmaf(ny, r.id.y, r.oid.y)),
                  fmaxf(__builtin_fmaf(nz, r.id.z, r.oid.z), 0.0f));
+#if RT_CLIP_ASM
+  // min of the three far planes and tmax_ray in two instructions (the compiler's fminf would first
+  // canonicalise tmax_ray, a loop-carried value, with an extra v_max per node)
+  asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
+      : "=&v"(s.tmax)
+      : "v"(__builtin_fmaf(fx, r.id.x, r.oid.x)), "v"(__builtin_fmaf(fy, r.id.y, r.oid.y)),
+        "v"(__builtin_fmaf(fz, r.id.z, r.oid.z)), "v"(tmax_ray));
+#else
   s.tmax = fminf(fminf(__builtin_fmaf(fx, r.id.x, r.oid.x), __builtin_fmaf(fy, r.id.y, r.oid.y)),
                  fminf(__builtin_fmaf(fz, r.id.z, r.oid.z), tmax_ray));
+#endif
   return s;
 }
 // lane masks straight from v_cmp (no bool materialisation): llvm.amdgcn.fcmp predicates
@@ -224,6 +236,28 @@ struct WaveStack {
   int sp = 0;
 };
 
+// Wave-packet loop with every option: VGPR or LDS stack and the counting run (RT_FRAME_STATS). The
+// production closest-hit / any-hit path is traverse_fast() below (same visit order, leaner per-node
+// code); this loop serves the counting run and the VGPR-stack A/B variant.
+// Knobs (A/B builds; results are identical either way):
+//   RT_ORDER_BITS       octant-specialised loops take the near child from the node's precomputed order
+//                       bit for the wave's octant (Node64::pad0, split-axis rule) instead of a lane vote
+//   RT_EXPERIMENT_SALU  timing experiment: N extra independent SALU per node step
+//   RT_EXPERIMENT_VALU  timing experiment: N extra independent VALU per node step
+#ifndef RT_ORDER_BITS
+#define RT_ORDER_BITS 0
+#endif
+#ifndef RT_FAST_LOOP
+#define RT_FAST_LOOP 1
+#endif
+#ifndef RT_EXPERIMENT_SALU
+#define RT_EXPERIMENT_SALU 0
+#endif
+#ifndef RT_EXPERIMENT_VALU
+#define RT_EXPERIMENT_VALU 0
+#endif
+#define RT_STR2(x) #x
+#define RT_STR(x) RT_STR2(x)
 template <bool ANY, bool STATS, bool STACK_LDS, int OCT = -1>
 __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                          uint32_t* lds_stack, uint32_t* cnt) {
@@ -235,6 +269,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
   uint64_t act = ballot(active);  // lanes still tracing (wave-uniform mask)
+  uint32_t exp_s = 0, exp_v = 0;  // RT_EXPERIMENT_SALU / _VALU sinks
   // one pop site and branch-free pushes keep the per-node control flow to the two uniform branches
   // (interior vs leaf, pop vs descend)
   for (;;) {
@@ -260,10 +295,24 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       }
 #endif
       const uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
-      // near child first by lane majority: each lane that needs a child votes for the one it enters
-      // first (covers m0 == 0 -> child 1 and m1 == 0 -> child 0)
-      const uint64_t v0 = m0 & (~m1 | mask_le(s0.tmin, s1.tmin));
-      const bool first0 = 2 * __popcll(v0) >= __popcll(m0 | m1);
+#if RT_EXPERIMENT_SALU > 0  // timing experiment only: N extra independent SALU per node step
+      exp_s = uniform(exp_s);
+      asm volatile(".rept " RT_STR(RT_EXPERIMENT_SALU) "\n\ts_add_u32 %0, %0, 1\n\t.endr" : "+s"(exp_s));
+#endif
+#if RT_EXPERIMENT_VALU > 0  // timing experiment only: N extra independent VALU per node step
+      asm volatile(".rept " RT_STR(RT_EXPERIMENT_VALU) "\n\tv_add_u32 %0, %0, 1\n\t.endr" : "+v"(exp_v));
+#endif
+      bool first0;
+      if (RT_ORDER_BITS && OCT >= 0) {
+        // the node's order bit for this octant, overridden when only one child is needed
+        const bool pref1 = (nd.pad0 >> (OCT & 7)) & 1u;
+        first0 = m1 == 0 || (m0 != 0 && !pref1);
+      } else {
+        // near child first by lane majority: each lane that needs a child votes for the one it enters
+        // first (covers m0 == 0 -> child 1 and m1 == 0 -> child 0)
+        const uint64_t v0 = m0 & (~m1 | mask_le(s0.tmin, s1.tmin));
+        first0 = 2 * __popcll(v0) >= __popcll(m0 | m1);
+      }
       const uint32_t far = first0 ? nd.child1 : nd.child0;
       // the far child is written above the top unconditionally and kept only when both are needed
       if (STACK_LDS) lds_stack[sp] = far;
@@ -307,6 +356,109 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       if (STATS) want = (flagstack >> sp) & 1;
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The production packet loop (LDS wave stack, no counting): the same visit order as traverse(), with
+// the per-node work arranged for the scalar unit, which is this kernel's tightest resource (measured:
+// one extra SALU per node step costs ~0.9% of the trace time, one extra VALU ~0.2%):
+//  * the descend / push / pop decision is one straight-line SALU block; a pop is signalled by the
+//    marker handle kPopMarker (leaf bit set, never a real leaf), so the interior loop needs one
+//    compare-and-branch per step and there is a single pop site;
+//  * lanes without a ray (closest hit) carry t_best = -1 and lanes whose shadow ray is blocked (any
+//    hit) carry a box-test limit of -1, so every box test fails for them and the masks need no
+//    "& active lanes" step.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kPopMarker = 0xFFFFFFFFu;
+
+template <bool ANY, int OCT>
+__device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                              uint32_t* lds_stack) {
+  if (P.n_nodes == 0) return;
+  int sp = 0;
+  uint32_t node = P.root;
+  uint64_t act = ballot(active);  // lanes still tracing: used by the triangle tests only
+  float tlim = active ? INFINITY : -1.0f;  // ANY: box-test limit (-1 once the lane is blocked)
+  if (!ANY && !active) h.t = -1.0f;
+  for (;;) {
+    while (!is_leaf(node)) {
+      const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
+      const float tcut = ANY ? tlim : h.t;
+      const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
+      const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+      const uint64_t m0 = mask_le(s0.tmin, s0.tmax), m1 = mask_le(s1.tmin, s1.tmax);
+      uint32_t nxt, far, ta, tb;
+      uint64_t tt;
+      // the far child is written above the top unconditionally and kept only when both are needed
+      // (the store takes the stack depth before the decision block updates it)
+      uint32_t* const slot = lds_stack + sp;
+      if (RT_ORDER_BITS && OCT >= 0) {
+        // near child from the node's order bit for this octant (Node64::pad0), overridden when only
+        // one child is needed
+        asm("s_cmp_lg_u64 %[m1], 0\n\t"
+            "s_cselect_b32 %[ta], %[bits], 0\n\t"
+            "s_bitcmp1_b32 %[ta], %[oct]\n\t"
+            "s_cselect_b32 %[nxt], %[c1], %[c0]\n\t"
+            "s_cselect_b32 %[far], %[c0], %[c1]\n\t"
+            "s_cmp_eq_u64 %[m0], 0\n\t"
+            "s_cselect_b32 %[nxt], %[c1], %[nxt]\n\t"
+            "s_cselect_b64 %[tt], 0, %[m1]\n\t"
+            "s_cmp_lg_u64 %[tt], 0\n\t"
+            "s_addc_u32 %[sp], %[sp], 0\n\t"
+            "s_or_b64 %[tt], %[m0], %[m1]\n\t"
+            "s_cselect_b32 %[nxt], %[nxt], -1"
+            : [nxt] "=&s"(nxt), [far] "=&s"(far), [sp] "+s"(sp), [ta] "=&s"(ta), [tt] "=&s"(tt)
+            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(nd.child0), [c1] "s"(nd.child1), [bits] "s"(nd.pad0),
+              [oct] "i"(OCT & 7)
+            : "scc");
+        (void)tb;
+        *slot = far;
+      } else {
+        // near child by lane majority: each lane that needs a child votes for the one it enters first
+        // (v0: lanes voting child 0; 2 * |v0| >= |m0 | m1| picks child 0, which also covers m1 == 0)
+        const uint64_t le = mask_le(s0.tmin, s1.tmin);
+        asm("s_orn2_b64 %[tt], %[le], %[m1]\n\t"
+            "s_and_b64 %[tt], %[tt], %[m0]\n\t"
+            "s_bcnt1_i32_b64 %[ta], %[tt]\n\t"
+            "s_or_b64 %[tt], %[m0], %[m1]\n\t"
+            "s_bcnt1_i32_b64 %[tb], %[tt]\n\t"
+            "s_lshl_b32 %[ta], %[ta], 1\n\t"
+            "s_cmp_ge_u32 %[ta], %[tb]\n\t"
+            "s_cselect_b32 %[nxt], %[c0], %[c1]\n\t"
+            "s_cselect_b32 %[far], %[c1], %[c0]\n\t"
+            "s_cmp_lg_u64 %[m0], 0\n\t"
+            "s_cselect_b64 %[tt], %[m1], 0\n\t"
+            "s_cmp_lg_u64 %[tt], 0\n\t"
+            "s_addc_u32 %[sp], %[sp], 0\n\t"
+            "s_cmp_eq_u32 %[tb], 0\n\t"
+            "s_cselect_b32 %[nxt], -1, %[nxt]"
+            : [nxt] "=&s"(nxt), [far] "=&s"(far), [sp] "+s"(sp), [ta] "=&s"(ta), [tb] "=&s"(tb),
+              [tt] "=&s"(tt)
+            : [m0] "s"(m0), [m1] "s"(m1), [le] "s"(le), [c0] "s"(nd.child0), [c1] "s"(nd.child1)
+            : "scc");
+        *slot = far;
+      }
+      node = nxt;
+    }
+    if (node != kPopMarker) {
+      // leaf: its triangles are fetched once per wave and tested by every lane
+      const uint32_t first = leaf_first(node), count = leaf_count(node);
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = sload_tri(P.tris, first + k);
+        test_tri<ANY>(P, tr, first + k, r, act, h, found);
+      }
+      if (ANY) {
+        active = active & !found;
+        act = ballot(active);
+        if (!act) break;
+        tlim = active ? INFINITY : -1.0f;
+      }
+    }
+    if (sp == 0) break;
+    sp--;
+    node = uniform(lds_stack[sp]);
+  }
+  if (!ANY && !active) h.t = INFINITY;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -563,6 +715,7 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
                                       WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   if (TRAV == TRAV_W4) traverse4<ANY, STATS>(P, r, active, h, found, L.stack[wv], L.mask[STATS ? wv : 0], cnt);
   else if (TRAV == TRAV_LANE) traverse_lane<ANY, STATS>(P, r, active, h, found, cnt);
+  else if (RT_FAST_LOOP && !STATS && TRAV == TRAV_B2_LDS) traverse_fast<ANY, -1>(P, r, active, h, found, L.stack[wv]);
   else traverse<ANY, STATS, TRAV == TRAV_B2_LDS>(P, r, active, h, found, L.stack[wv], cnt);
 }
 
@@ -582,6 +735,18 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
                    sz = ballot(__float_as_uint(r.id.z) >> 31) & act;
     if ((sx == 0 || sx == act) && (sy == 0 || sy == act) && (sz == 0 || sz == act)) {
       const int oct = (sx ? 1 : 0) | (sy ? 2 : 0) | (sz ? 4 : 0);
+      if (RT_FAST_LOOP && !STATS && SL) {
+        switch (oct) {
+          case 0: traverse_fast<false, 0>(P, r, active, h, found, L.stack[wv]); return;
+          case 1: traverse_fast<false, 1>(P, r, active, h, found, L.stack[wv]); return;
+          case 2: traverse_fast<false, 2>(P, r, active, h, found, L.stack[wv]); return;
+          case 3: traverse_fast<false, 3>(P, r, active, h, found, L.stack[wv]); return;
+          case 4: traverse_fast<false, 4>(P, r, active, h, found, L.stack[wv]); return;
+          case 5: traverse_fast<false, 5>(P, r, active, h, found, L.stack[wv]); return;
+          case 6: traverse_fast<false, 6>(P, r, active, h, found, L.stack[wv]); return;
+          default: traverse_fast<false, 7>(P, r, active, h, found, L.stack[wv]); return;
+        }
+      }
       switch (oct) {
         case 0: traverse<false, STATS, SL, 0>(P, r, active, h, found, L.stack[wv], cnt); return;
         case 1: traverse<false, STATS, SL, 1>(P, r, active, h, found, L.stack[wv], cnt); return;
@@ -711,16 +876,28 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   PixelCoord c;
   c.lane = threadIdx.x & 63;
   int nb, b;
+  int bid = (int)blockIdx.x;
+  if (P.xcd_remap >= 2) {
+    // chunked XCD order: blocks b and b + 8 share an XCD, so the k-th block of XCD x takes position
+    // (k / C) * 8C + x C + k % C -- each XCD receives runs of C consecutive blocks (for one-wave
+    // blocks, the four quarters of a tile and its row neighbours) while the runs still interleave
+    // over the frame (load balance). The trailing partial group keeps the identity order.
+    const int C = P.xcd_remap, G = 8 * C, full = ((int)gridDim.x / G) * G;
+    if (bid < full) {
+      const int x = bid & 7, k = bid >> 3;
+      bid = (k / C) * G + x * C + (k % C);
+    }
+  }
   if (WPB == 4) {
     c.wv = (int)uniform(threadIdx.x >> 6);
     c.slot = c.wv;
     nb = (int)gridDim.x;
-    b = (int)blockIdx.x;
+    b = bid;
   } else {
-    c.wv = (int)(blockIdx.x & 3);
+    c.wv = bid & 3;
     c.slot = 0;
     nb = (int)(gridDim.x >> 2);
-    b = (int)(blockIdx.x >> 2);
+    b = bid >> 2;
   }
   c.qw = b * 4 + c.wv;
   int L = b;
@@ -1559,7 +1736,8 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 
 // variant bits (debug knob RT_KERNEL_VARIANT, for A/B measurements; 0 = the measured-best default):
 // 1 = binary nodes + lane-register (VGPR) stack, 2 = 4-wide quantised nodes (when the scene has
-// them), 4 = XCD-contiguous tile order, 16 = FULL as the stage pipeline (k_full_*) instead of one
+// them), 4 = XCD-contiguous tile order, 512 / 1024 / 1536 = block runs of 4 / 16 / plain dispatch order
+// instead of the default 64-block runs per XCD, 16 = FULL as the stage pipeline (k_full_*) instead of one
 // kernel; with 16: 32 / 64 / 128 = per-lane traversal for the reflection rays / the shadow rays of
 // reflection hits / the shadow rays of primary hits. Default: binary nodes + LDS stack, FULL as one
 // kernel (k_render_full).
@@ -1736,7 +1914,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     if ((rc = ensure_full(slot, npad))) return rc;
     bind_full(slot, P);
   }
-  P.xcd_remap = (variant & 4) ? 1 : 0;
+  // block order: chunked XCD order with runs of 64 blocks by default (measured -4% trace time on C3:
+  // the quarters of a tile and their row neighbours share an XCD's L2); variant bits 512 / 1024 select
+  // runs of 4 / 16 blocks, 1536 the plain dispatch order, 4 one contiguous tile range per XCD
+  {
+    const int sel = (variant >> 9) & 3;
+    P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? 64 : sel == 1 ? 4 : sel == 2 ? 16 : 0);
+  }
   const int trav = pick_trav(P, variant);
   if (s->ev_used + 3 > s->ev_pool.size()) {
     if (s->ev_pool.size() >= 3 * 2048) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }

@@ -960,6 +960,28 @@ void face_records(const HostScene& hs, std::vector<TriRec64>& out) {
   });
 }
 
+// Traversal-order hint of a node for waves whose rays share one direction octant (bit k of the octant:
+// axis k negative): bit `oct` set = visit child 1 first. Split-axis rule: along the axis on which the
+// children's centres are furthest apart, the child on the ray's entry side comes first. Only the visit
+// order depends on it, never a result (every needed child is still visited).
+uint32_t octant_order(const Node64& nd) {
+  const float c0[3] = {nd.c0lx + nd.c0hx, nd.c0ly + nd.c0hy, nd.c0lz + nd.c0hz};
+  const float c1[3] = {nd.c1lx + nd.c1hx, nd.c1ly + nd.c1hy, nd.c1lz + nd.c1hz};
+  int axis = 0;
+  float best = -1.0f;
+  for (int k = 0; k < 3; k++) {
+    const float sep = std::fabs(c1[k] - c0[k]);
+    if (sep > best) best = sep, axis = k;
+  }
+  const bool c1_low = c1[axis] < c0[axis];
+  uint32_t bits = 0;
+  for (uint32_t oct = 0; oct < 8; oct++) {
+    const bool negative = (oct >> axis) & 1u;
+    if (c1_low != negative) bits |= 1u << oct;
+  }
+  return bits;
+}
+
 // interior nodes re-laid out depth-first (near child first) from `root`; unreferenced nodes dropped;
 // sets hs.nodes, hs.root = 0, hs.depth (levels of interior nodes + the leaf level)
 void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) {
@@ -986,7 +1008,10 @@ void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) 
   hs.root = 0;
   hs.depth = depth;
   hs.leaves = 0;
-  for (const Node64& nd : hs.nodes) hs.leaves += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
+  for (Node64& nd : hs.nodes) {
+    hs.leaves += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
+    nd.pad0 = octant_order(nd);
+  }
 }
 
 void build_bvh(HostScene& hs, int leaf_size) {
@@ -1192,6 +1217,13 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   if (d->n_vertices < 0 || d->n_faces < 0 || (d->n_faces && (!d->face_vertex_ids || !d->face_normals || !d->face_material_ids)) ||
       (d->n_vertices && (!d->vertices || !d->vertex_normals))) {
     rt::set_error("rt_scene_create: invalid mesh description");
+    return RT_ERR_INVALID;
+  }
+  // leaf handles hold the first triangle slot in 27 bits; the all-ones handle is the traversal's pop
+  // marker, so slots stay below kLeafFirstMask - kMaxLeaf
+  if ((int64_t)d->n_faces > (int64_t)rt::kLeafFirstMask - rt::kMaxLeaf) {
+    rt::set_error("rt_scene_create: %d faces exceed the %u-face limit", d->n_faces,
+                  rt::kLeafFirstMask - rt::kMaxLeaf);
     return RT_ERR_INVALID;
   }
   auto t0 = std::chrono::steady_clock::now();

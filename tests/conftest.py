@@ -4,6 +4,12 @@ import sys
 
 import pytest
 
+# torch first: it ships its own HIP runtime, and the process must use ONE copy of libamdhip64. When
+# torch is imported after the library has already loaded the system runtime, torch's device init
+# fails ("No HIP GPUs are available"), so the GPU tests that hand torch buffers to the library
+# (shard gather) would depend on collection order.
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "ray-tracing-project_amd")
 SCENES = os.path.join(ROOT, "scenes")

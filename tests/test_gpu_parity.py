@@ -188,7 +188,7 @@ def test_stats_counting_run(rt, soup):
     assert st["wave_node_fetches"] * 16 < st["node_visits"]  # coherence: one fetch serves many rays
 
 
-VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "full-pipeline": 16, "pipeline-lane-refl": 48,
+VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-pipeline": 16, "pipeline-lane-refl": 48,
             "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256}
 
 
