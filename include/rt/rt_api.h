@@ -121,7 +121,8 @@ void rt_scene_opts_default(rt_scene_opts* o);
 typedef struct rt_scene rt_scene;
 
 /* Builds the reference's flat box partition (generateBoundingBoxes, flyscene.cpp:399-428, whose box
- * order defines closest-hit tie-breaking) and the traversal BVH, then uploads both. */
+ * order defines closest-hit tie-breaking) and the traversal BVH, then uploads both. At most 2^25 - 1
+ * faces (node and triangle records are addressed by 32-bit byte offsets); more: RT_ERR_INVALID. */
 int rt_scene_create(const rt_mesh_desc* mesh, const rt_scene_opts* opts, rt_scene** out);
 void rt_scene_destroy(rt_scene* s);
 

@@ -52,13 +52,44 @@ template <typename T>
 __device__ __forceinline__ T sload64(const T* base, uint32_t i) {
   static_assert(sizeof(T) == 64, "64-byte records");
   const uint32_t off = __builtin_amdgcn_readfirstlane(i) * 64u;  // byte offset in an SGPR (< 4 GiB)
+  // the base is uniform, but inside divergent regions (FULL mode's secondary packets) the compiler
+  // may keep it in VGPRs; readfirstlane folds away when it is already scalar
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
   i16v v;
-  asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off) : "memory");
+  asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(bs), "s"(off) : "memory");
   T r;
   __builtin_memcpy(&r, &v, 64);
   return r;
 }
 __device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t i) { return sload64(base, i); }
+// The same node fetch, then a prefetch of both children's records into the scalar cache, issued the
+// moment the node has arrived so that it overlaps this node's box tests: one dword each pulls in the
+// 64-B line. pad0 / pad1 (loaded alongside, same line) are the byte offsets from the nodes base of
+// child 0 / 1's node record or, for a leaf child, of its first triangle record (device_upload).
+// pf0 / pf1 receive the prefetched dwords: the caller keeps them live until an s_waitcnt
+// lgkmcnt(0) has retired the loads (the hardware writes them whenever the data returns).
+__device__ __forceinline__ Node64 sload_node_pf(const Node64* base, uint32_t i, uint32_t& pf0, uint32_t& pf1) {
+  const uint32_t off = __builtin_amdgcn_readfirstlane(i) * 64u;
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  i16v v;
+  asm volatile(
+      "s_load_dwordx16 %0, %3, %4\n\t"
+      "s_load_dword %1, %3, %4 offset:0x38\n\t"
+      "s_load_dword %2, %3, %4 offset:0x3c\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_load_dword %1, %3, %1\n\t"
+      "s_load_dword %2, %3, %2"
+      : "=&s"(v), "=&s"(pf0), "=&s"(pf1)
+      : "s"(bs), "s"(off)
+      : "memory");
+  Node64 r;
+  __builtin_memcpy(&r, &v, 64);
+  return r;
+}
 __device__ __forceinline__ TriRec64 sload_tri(const TriRec64* base, uint32_t i) { return sload64(base, i); }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -256,6 +287,12 @@ struct WaveStack {
 #ifndef RT_EXPERIMENT_VALU
 #define RT_EXPERIMENT_VALU 0
 #endif
+// RT_PREFETCH: the fast loop prefetches both children's records into the scalar cache (Node64::pad0/1
+// then hold prefetch offsets instead of the order bits)
+#ifndef RT_PREFETCH
+#define RT_PREFETCH 1
+#endif
+static_assert(!(RT_PREFETCH && RT_ORDER_BITS), "RT_PREFETCH reuses Node64::pad0 (the order bits)");
 #define RT_STR2(x) #x
 #define RT_STR(x) RT_STR2(x)
 template <bool ANY, bool STATS, bool STACK_LDS, int OCT = -1>
@@ -316,7 +353,10 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       const uint32_t far = first0 ? nd.child1 : nd.child0;
       // the far child is written above the top unconditionally and kept only when both are needed
       if (STACK_LDS) lds_stack[sp] = far;
-      else asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(stackv) : "s"(far), "s"(sp) : "m0");
+      else asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
+                        : "+v"(stackv)
+                        : "s"(uniform(far)), "s"(uniform((uint32_t)sp))
+                        : "m0");
       if (STATS) {
         const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
         const bool wf = first0 ? h1 : h0;
@@ -382,7 +422,12 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
   if (!ANY && !active) h.t = -1.0f;
   for (;;) {
     while (!is_leaf(node)) {
+#if RT_PREFETCH
+      uint32_t pf0, pf1;
+      const Node64 nd = sload_node_pf(P.nodes, node, pf0, pf1);
+#else
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
+#endif
       const float tcut = ANY ? tlim : h.t;
       const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
       const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
@@ -391,6 +436,10 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
       uint64_t tt;
       // the far child is written above the top unconditionally and kept only when both are needed
       // (the store takes the stack depth before the decision block updates it)
+      // (uniform(): inside FULL mode's divergent regions the compiler may otherwise hand the scalar
+      // decision block values it keeps in VGPRs; readfirstlane folds away on SGPR values)
+      sp = (int)uniform((uint32_t)sp);
+      const uint32_t c0 = uniform(nd.child0), c1 = uniform(nd.child1);
       uint32_t* const slot = lds_stack + sp;
       if (RT_ORDER_BITS && OCT >= 0) {
         // near child from the node's order bit for this octant (Node64::pad0), overridden when only
@@ -408,7 +457,7 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
             "s_or_b64 %[tt], %[m0], %[m1]\n\t"
             "s_cselect_b32 %[nxt], %[nxt], -1"
             : [nxt] "=&s"(nxt), [far] "=&s"(far), [sp] "+s"(sp), [ta] "=&s"(ta), [tt] "=&s"(tt)
-            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(nd.child0), [c1] "s"(nd.child1), [bits] "s"(nd.pad0),
+            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [bits] "s"(uniform(nd.pad0)),
               [oct] "i"(OCT & 7)
             : "scc");
         (void)tb;
@@ -434,19 +483,53 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
             "s_cselect_b32 %[nxt], -1, %[nxt]"
             : [nxt] "=&s"(nxt), [far] "=&s"(far), [sp] "+s"(sp), [ta] "=&s"(ta), [tb] "=&s"(tb),
               [tt] "=&s"(tt)
-            : [m0] "s"(m0), [m1] "s"(m1), [le] "s"(le), [c0] "s"(nd.child0), [c1] "s"(nd.child1)
+            : [m0] "s"(m0), [m1] "s"(m1), [le] "s"(le), [c0] "s"(c0), [c1] "s"(c1)
             : "scc");
         *slot = far;
       }
       node = nxt;
+#if RT_PREFETCH
+      // the prefetch registers stay allocated until their data has landed (the hardware writes them
+      // whenever the load returns); the next record load then hits the scalar cache
+      asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(pf0), "s"(pf1) : "memory");
+#endif
     }
     if (node != kPopMarker) {
       // leaf: its triangles are fetched once per wave and tested by every lane
       const uint32_t first = leaf_first(node), count = leaf_count(node);
+#if RT_PREFETCH >= 2
+      // triangles 1..3 of the leaf requested together with triangle 0 (the parent prefetched
+      // triangle 0), so the per-triangle fetches of the loop below hit the scalar cache
+      uint32_t q1, q2, q3;
+      {
+        const uint32_t last = first + count - 1;
+        asm volatile("s_load_dword %0, %3, %4\n\ts_load_dword %1, %3, %5\n\ts_load_dword %2, %3, %6"
+                     : "=&s"(q1), "=&s"(q2), "=&s"(q3)
+                     : "s"(P.tris), "s"(uniform(min(first + 1, last) * 64u)), "s"(uniform(min(first + 2, last) * 64u)),
+                       "s"(uniform(min(first + 3, last) * 64u))
+                     : "memory");
+      }
+#endif
+#if RT_PREFETCH >= 3
+      // the record the pop after this leaf will fetch (the stack top), requested while the
+      // triangles are tested (its handle from the LDS stack; a leaf's first triangle for a leaf)
+      uint32_t q4;
+      {
+        const uint32_t top = uniform(lds_stack[sp > 0 ? sp - 1 : 0]);
+        uint32_t off = 64u * (is_leaf(top) ? (uint32_t)P.n_nodes + leaf_first(top) : top);
+        off = sp > 0 ? off : 0u;
+        asm volatile("s_load_dword %0, %1, %2" : "=&s"(q4) : "s"(P.nodes), "s"(uniform(off)) : "memory");
+      }
+#endif
       for (uint32_t k = 0; k < count; k++) {
         const TriRec64 tr = sload_tri(P.tris, first + k);
         test_tri<ANY>(P, tr, first + k, r, act, h, found);
       }
+#if RT_PREFETCH >= 3
+      asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(q1), "s"(q2), "s"(q3), "s"(q4) : "memory");
+#elif RT_PREFETCH >= 2
+      asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(q1), "s"(q2), "s"(q3) : "memory");
+#endif
       if (ANY) {
         active = active & !found;
         act = ballot(active);
@@ -724,10 +807,9 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
 #ifndef RT_OCT_SPECIALIZE
 #define RT_OCT_SPECIALIZE 1
 #endif
-template <bool STATS, int TRAV>
-__device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& r, bool active, Hit& h,
-                                                  WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
-  bool found = false;
+template <bool ANY, bool STATS, int TRAV>
+__device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                          WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   if (RT_OCT_SPECIALIZE && (TRAV == TRAV_B2_LDS || TRAV == TRAV_B2_VGPR)) {
     constexpr bool SL = TRAV == TRAV_B2_LDS;
     const uint64_t act = ballot(active);
@@ -737,29 +819,47 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
       const int oct = (sx ? 1 : 0) | (sy ? 2 : 0) | (sz ? 4 : 0);
       if (RT_FAST_LOOP && !STATS && SL) {
         switch (oct) {
-          case 0: traverse_fast<false, 0>(P, r, active, h, found, L.stack[wv]); return;
-          case 1: traverse_fast<false, 1>(P, r, active, h, found, L.stack[wv]); return;
-          case 2: traverse_fast<false, 2>(P, r, active, h, found, L.stack[wv]); return;
-          case 3: traverse_fast<false, 3>(P, r, active, h, found, L.stack[wv]); return;
-          case 4: traverse_fast<false, 4>(P, r, active, h, found, L.stack[wv]); return;
-          case 5: traverse_fast<false, 5>(P, r, active, h, found, L.stack[wv]); return;
-          case 6: traverse_fast<false, 6>(P, r, active, h, found, L.stack[wv]); return;
-          default: traverse_fast<false, 7>(P, r, active, h, found, L.stack[wv]); return;
+          case 0: traverse_fast<ANY, 0>(P, r, active, h, found, L.stack[wv]); return;
+          case 1: traverse_fast<ANY, 1>(P, r, active, h, found, L.stack[wv]); return;
+          case 2: traverse_fast<ANY, 2>(P, r, active, h, found, L.stack[wv]); return;
+          case 3: traverse_fast<ANY, 3>(P, r, active, h, found, L.stack[wv]); return;
+          case 4: traverse_fast<ANY, 4>(P, r, active, h, found, L.stack[wv]); return;
+          case 5: traverse_fast<ANY, 5>(P, r, active, h, found, L.stack[wv]); return;
+          case 6: traverse_fast<ANY, 6>(P, r, active, h, found, L.stack[wv]); return;
+          default: traverse_fast<ANY, 7>(P, r, active, h, found, L.stack[wv]); return;
         }
       }
       switch (oct) {
-        case 0: traverse<false, STATS, SL, 0>(P, r, active, h, found, L.stack[wv], cnt); return;
-        case 1: traverse<false, STATS, SL, 1>(P, r, active, h, found, L.stack[wv], cnt); return;
-        case 2: traverse<false, STATS, SL, 2>(P, r, active, h, found, L.stack[wv], cnt); return;
-        case 3: traverse<false, STATS, SL, 3>(P, r, active, h, found, L.stack[wv], cnt); return;
-        case 4: traverse<false, STATS, SL, 4>(P, r, active, h, found, L.stack[wv], cnt); return;
-        case 5: traverse<false, STATS, SL, 5>(P, r, active, h, found, L.stack[wv], cnt); return;
-        case 6: traverse<false, STATS, SL, 6>(P, r, active, h, found, L.stack[wv], cnt); return;
-        default: traverse<false, STATS, SL, 7>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 0: traverse<ANY, STATS, SL, 0>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 1: traverse<ANY, STATS, SL, 1>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 2: traverse<ANY, STATS, SL, 2>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 3: traverse<ANY, STATS, SL, 3>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 4: traverse<ANY, STATS, SL, 4>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 5: traverse<ANY, STATS, SL, 5>(P, r, active, h, found, L.stack[wv], cnt); return;
+        case 6: traverse<ANY, STATS, SL, 6>(P, r, active, h, found, L.stack[wv], cnt); return;
+        default: traverse<ANY, STATS, SL, 7>(P, r, active, h, found, L.stack[wv], cnt); return;
       }
     }
   }
-  trace<false, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
+  trace<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
+}
+template <bool STATS, int TRAV>
+__device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& r, bool active, Hit& h,
+                                                  WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
+  bool found = false;
+  trace_oct<false, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
+}
+
+// FULL mode: primary, reflection and shadow packets also take the octant-specialised loops when the
+// wave's rays share an octant (A/B knob)
+#ifndef RT_FULL_OCT
+#define RT_FULL_OCT 0
+#endif
+template <bool ANY, bool STATS, int TRAV>
+__device__ __forceinline__ void trace_full_ray(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                               WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
+  if (RT_FULL_OCT) trace_oct<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
+  else trace<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -848,7 +948,7 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       setup_cull(sr);
       Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if (STATS && lane_hit) cnt[ST_TOTAL]++;
-      trace<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
+      trace_full_ray<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
     }
     f3 c{0.0f, 0.0f, 0.0f};
     if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
@@ -1078,7 +1178,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
                                          uint32_t* cnt, Hit& h, uint32_t& face0) {
   h = Hit{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  trace<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
+  trace_full_ray<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
   const bool hit0 = active && h.t != INFINITY;
   if (STATS && hit0) cnt[ST_HITS]++;
 
@@ -1107,7 +1207,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   setup_cull(rr);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  trace<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
+  trace_full_ray<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
   hi1.mat = -1;
@@ -1305,7 +1405,7 @@ void k_full_shadow(FrameParams P, int pass) {
     Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
     bool blocked = false;
     if (STATS && L.act) cnt[ST_TOTAL]++;
-    trace<true, STATS, TRAV>(P.sc, sr, L.act, hh, blocked, lds, wv, cnt);
+    trace_full_ray<true, STATS, TRAV>(P.sc, sr, L.act, hh, blocked, lds, wv, cnt);
     bits |= (blocked ? 1u : 0u) << l;
   }
   if (L.act) (pass ? P.blk1 : P.blk0)[pix] = bits;
@@ -1336,7 +1436,7 @@ void k_full_refl(FrameParams P) {
   if (STATS && L.act) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  trace<false, STATS, TRAV>(P.sc, rr, L.act, h1, dummy, lds, wv, cnt);
+  trace_full_ray<false, STATS, TRAV>(P.sc, rr, L.act, h1, dummy, lds, wv, cnt);
   if (L.act) P.hits1[pix] = make_uint2(__float_as_uint(h1.t), h1.slot);
   const uint32_t nh = (uint32_t)__popcll(ballot(L.act && h1.t != INFINITY));
   if (lane_id() == 0) P.wcount1[L.w] = nh;
@@ -1605,9 +1705,29 @@ int device_upload(rt_scene* s) {
   int64_t& tot = s->device_bytes;
   tot = 0;
   int rc;
-  if ((rc = dalloc_copy(&s->d_nodes, hs.nodes.data(), hs.nodes.size() * sizeof(Node64), tot))) return rc;
+  {
+    // BVH nodes and triangle records share one allocation (triangles right after the nodes), so one
+    // base plus a 32-bit byte offset reaches either: with RT_PREFETCH each uploaded node's pad0 / pad1
+    // hold the offsets of its children's records (a leaf child: its first triangle)
+    const size_t nn = hs.nodes.size(), nt = hs.tris.size();
+    const size_t bytes = (nn + nt) * 64;
+    if (bytes > 0xFFFFFFFFull) {  // cannot happen below kMaxFaces (rt_scene_create checks it)
+      set_error("scene records exceed 4 GiB (%zu nodes, %zu triangles)", nn, nt);
+      return RT_ERR_INVALID;
+    }
+    if ((rc = dalloc_copy(&s->d_nodes, nullptr, bytes, tot))) return rc;
+    std::vector<Node64> nodes(hs.nodes);
+    if (RT_PREFETCH) {
+      auto pf = [&](uint32_t c) -> uint32_t {
+        return (uint32_t)(64 * (is_leaf(c) ? nn + leaf_first(c) : (size_t)c));
+      };
+      for (Node64& nd : nodes) { nd.pad0 = pf(nd.child0); nd.pad1 = pf(nd.child1); }
+    }
+    if (nn) HIPCHECK(hipMemcpy(s->d_nodes, nodes.data(), nn * 64, hipMemcpyHostToDevice));
+    s->d_tris = reinterpret_cast<TriRec64*>(s->d_nodes + nn);
+    if (nt) HIPCHECK(hipMemcpy(s->d_tris, hs.tris.data(), nt * 64, hipMemcpyHostToDevice));
+  }
   if ((rc = dalloc_copy(&s->d_nodes4, hs.nodes4.data(), hs.nodes4.size() * sizeof(Node4Q), tot))) return rc;
-  if ((rc = dalloc_copy(&s->d_tris, hs.tris.data(), hs.tris.size() * sizeof(TriRec64), tot))) return rc;
   std::vector<uint32_t> fshade(4 * (size_t)hs.nf);
   for (int32_t f = 0; f < hs.nf; f++) {
     fshade[4 * f + 0] = hs.fidx[3 * f + 0];
@@ -1643,7 +1763,7 @@ void device_release(rt_scene* s) {
   (void)hipSetDevice(s->device);
   for (int k = 0; k < s->n_slots; k++)
     if (s->slots[k].stream) (void)hipStreamSynchronize((hipStream_t)s->slots[k].stream);
-  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_tris, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats};
+  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats};  // d_tris: inside d_nodes
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (int k = 0; k < s->n_slots; k++) {

@@ -1219,11 +1219,11 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     rt::set_error("rt_scene_create: invalid mesh description");
     return RT_ERR_INVALID;
   }
-  // leaf handles hold the first triangle slot in 27 bits; the all-ones handle is the traversal's pop
-  // marker, so slots stay below kLeafFirstMask - kMaxLeaf
-  if ((int64_t)d->n_faces > (int64_t)rt::kLeafFirstMask - rt::kMaxLeaf) {
-    rt::set_error("rt_scene_create: %d faces exceed the %u-face limit", d->n_faces,
-                  rt::kLeafFirstMask - rt::kMaxLeaf);
+  // leaf handles hold the first triangle slot in 27 bits (the all-ones handle is the traversal's pop
+  // marker) and records are addressed by 32-bit byte offsets (kMaxFaces, rt_internal.h)
+  static_assert(rt::kMaxFaces < rt::kLeafFirstMask - rt::kMaxLeaf, "leaf handle range");
+  if ((int64_t)d->n_faces > (int64_t)rt::kMaxFaces) {
+    rt::set_error("rt_scene_create: %d faces exceed the %u-face limit", d->n_faces, rt::kMaxFaces);
     return RT_ERR_INVALID;
   }
   auto t0 = std::chrono::steady_clock::now();

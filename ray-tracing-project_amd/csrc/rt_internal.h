@@ -26,6 +26,10 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kLeafCountShift = 27;          // 4 bits: count - 1 (1..16 triangles)
 constexpr uint32_t kLeafFirstMask = (1u << 27) - 1;  // first triangle slot (< 134M)
 constexpr int kMaxLeaf = 16;
+// Node and triangle records are addressed by 32-bit byte offsets from one base (scalar loads with an
+// SGPR offset; nodes and triangles share one allocation), so nodes + triangles < 2^26 records: with
+// at most n_faces - 1 interior nodes that is n_faces < 2^25
+constexpr uint32_t kMaxFaces = (1u << 25) - 1;
 constexpr int kMaxDepth = 60;  // wave stack holds 64 entries; occupancy <= depth
 // TriRec64::box bit 31: the triangle's interpolated normal can never be the zero vector (see
 // rt_host.cpp safe_normal()), so calculateDistance's norm()==0 rejection never fires for it
