@@ -292,6 +292,9 @@ struct WaveStack {
 #ifndef RT_PREFETCH
 #define RT_PREFETCH 1
 #endif
+#ifndef RT_PREFETCH_PADLOAD  // 1: offsets re-loaded inside the node-load asm (0: tie-ordered separate asm, measured ±0.5%)
+#define RT_PREFETCH_PADLOAD 1
+#endif
 static_assert(!(RT_PREFETCH && RT_ORDER_BITS), "RT_PREFETCH reuses Node64::pad0 (the order bits)");
 #define RT_STR2(x) #x
 #define RT_STR(x) RT_STR2(x)
@@ -424,7 +427,17 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
     while (!is_leaf(node)) {
 #if RT_PREFETCH
       uint32_t pf0, pf1;
+#if RT_PREFETCH_PADLOAD
       const Node64 nd = sload_node_pf(P.nodes, node, pf0, pf1);
+#else
+      Node64 nd = sload_node(P.nodes, node);
+      // both children's records into the scalar cache, issued the moment the node has arrived: the
+      // box coordinates are declared read-write operands so the box tests cannot be scheduled above it
+      asm volatile("s_load_dword %0, %4, %5\n\ts_load_dword %1, %4, %6"
+                   : "=&s"(pf0), "=&s"(pf1), "+s"(nd.c0lx), "+s"(nd.c1lx)
+                   : "s"(P.nodes), "s"(nd.pad0), "s"(nd.pad1)
+                   : "memory");
+#endif
 #else
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
 #endif
