@@ -163,22 +163,26 @@ void compute_normals(rt_mesh* m, const std::vector<std::vector<uint32_t>>& group
 int finish_mesh(rt_mesh* m, const std::vector<std::vector<uint32_t>>& groups, const std::vector<int32_t>& gmat,
                 bool have_vn) {
   const size_t nv = m->v4.size() / 4;
+  // validate every index group before anything indexes with it (computeNormals included: the
+  // reference reads and writes out of bounds here)
+  if (nv > 0)
+    for (const auto& ix : groups) {
+      if (ix.size() % 3 != 0) {
+        rt::set_error("index group of %zu indices is not a multiple of 3 (reference reads out of bounds)", ix.size());
+        return RT_ERR_INVALID;
+      }
+      for (uint32_t id : ix)
+        if (id >= nv) { rt::set_error("face vertex index %u out of range", id + 1); return RT_ERR_INVALID; }
+    }
   load_vertices(m);
-  if (!have_vn) compute_normals(m, groups);
+  if (!have_vn && nv > 0) compute_normals(m, groups);  // no vertices: no faces either (below)
   m->fidx.clear(); m->fn3.clear(); m->fmat.clear();
   auto V = [&](uint32_t i) { return f3{m->v4[4 * i], m->v4[4 * i + 1], m->v4[4 * i + 2]}; };
   if (nv > 0)
     for (size_t g = 0; g < groups.size(); g++) {
       const auto& ix = groups[g];
-      if (ix.size() % 3 != 0) {
-        rt::set_error("index group of %zu indices is not a multiple of 3 (reference reads out of bounds)", ix.size());
-        return RT_ERR_INVALID;
-      }
       for (size_t i = 0; i < ix.size(); i += 3) {
-        for (int k = 0; k < 3; k++) {
-          if (ix[i + k] >= nv) { rt::set_error("face vertex index %u out of range", ix[i + k] + 1); return RT_ERR_INVALID; }
-          m->fidx.push_back(ix[i + k]);
-        }
+        for (int k = 0; k < 3; k++) m->fidx.push_back(ix[i + k]);
         m->fmat.push_back(gmat[g]);
         f3 v1 = rt::normalized(rt::sub(V(ix[i + 2]), V(ix[i])));
         f3 v0 = rt::normalized(rt::sub(V(ix[i + 1]), V(ix[i])));
@@ -377,13 +381,16 @@ extern "C" int rt_write_ppm(const char* path, const float* rgb, int32_t W, int32
 // without per-number formatting calls: a table of the 256 "%d " strings
 extern "C" int rt_write_ppm_rgb8(const char* path, const uint8_t* rgb8, int32_t W, int32_t H) {
   if (!path || !rgb8 || W <= 0 || H <= 0) { rt::set_error("rt_write_ppm_rgb8: invalid arguments"); return RT_ERR_INVALID; }
-  static char tab[256][4];
-  static uint8_t len[256];
-  static bool init = false;
-  if (!init) {
-    for (int v = 0; v < 256; v++) len[v] = (uint8_t)snprintf(tab[v], 5, "%d ", v);
-    init = true;
-  }
+  struct Tab {
+    char s[256][5];  // "255 " plus the terminator
+    uint8_t len[256];
+    Tab() {
+      for (int v = 0; v < 256; v++) len[v] = (uint8_t)snprintf(s[v], sizeof s[v], "%d ", v);
+    }
+  };
+  static const Tab t;  // thread-safe one-time initialisation
+  const auto& tab = t.s;
+  const auto& len = t.len;
   std::string out;
   out.reserve((size_t)W * H * 12 + 64);
   out += "P3\n" + std::to_string(W) + " " + std::to_string(H) + "\n255\n";

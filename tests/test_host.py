@@ -161,9 +161,27 @@ def test_invalid_inputs_rejected(rt, tmp_path):
     bad.write_text("v 0 0 0\nv 1 0 0\nf 1 2\n")
     with pytest.raises(rt.RTError, match="multiple of 3"):
         rt.Mesh.load_obj(str(bad))
-    bad.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 9\n")
-    with pytest.raises(rt.RTError, match="out of range"):
-        rt.Mesh.load_obj(str(bad))
+    # out-of-range indices are rejected before anything indexes with them (the reference's
+    # computeNormals would write out of bounds: objimporter.hpp:81-106)
+    for faces in ("f 1 2 9", "f 0 1 2", "f -1 2 3"):
+        bad.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\n" + faces + "\n")
+        with pytest.raises(rt.RTError, match="out of range"):
+            rt.Mesh.load_obj(str(bad))
+
+
+def test_host_code_under_sanitizers():
+    """Host entry points (OBJ ingest incl. malformed files, host-only scenes, BVH validation, the scene
+    cache with truncated / bit-flipped files, PPM writers, lights) under AddressSanitizer + UBSan +
+    LeakSanitizer: tools/asan/run.sh rebuilds the host translation units instrumented and fails on any
+    report."""
+    import shutil
+    import subprocess
+    if not os.path.exists("/opt/rocm/bin/hipcc") or shutil.which("make") is None:
+        pytest.skip("needs hipcc + make")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(root, "tools", "asan", "run.sh")], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and "host_asan: ok" in r.stdout, (r.stdout[-2000:] + r.stderr[-4000:])
 
 
 @pytest.mark.parametrize("name", ["cube", "bunny"])
