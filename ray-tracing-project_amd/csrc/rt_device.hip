@@ -1250,6 +1250,67 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   return col;
 }
 
+// The same traceRay(o, d, 0) as a loop over the two depths, so that the closest-hit and the any-hit
+// traversal each appear once in the kernel instead of twice (A/B knob RT_FULL_LOOP). Same expressions
+// in the same order as trace_full above, hence the same bits.
+#ifndef RT_FULL_LOOP
+#define RT_FULL_LOOP 0
+#endif
+template <bool STATS, int TRAV>
+__device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r, bool active, WaveLds<TRAV, STATS>& lds,
+                                              int wv, uint32_t* cnt, Hit& h0, uint32_t& face0) {
+  MatState st = load_mat(P.defmat);
+  Ray cur = r;
+  bool act = active, hit0 = false;
+  f3 direct0{0.0f, 0.0f, 0.0f}, refl{0.0f, 0.0f, 0.0f};
+  face0 = 0xFFFFFFFFu;
+#pragma clang loop unroll(disable)
+  for (int depth = 0; depth < 2; depth++) {
+    Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    bool dummy = false;
+    trace_full_ray<false, STATS, TRAV>(P.sc, cur, act, h, dummy, lds, wv, cnt);
+    const bool hit = act && h.t != INFINITY;
+    if (STATS && depth == 0 && hit) cnt[ST_HITS]++;
+    HitInfo hi;
+    hi.mat = -1;
+    hi.face = 0xFFFFFFFFu;
+    hi.p = f3{0.0f, 0.0f, 0.0f};
+    hi.n = f3{0.0f, 0.0f, 0.0f};
+    if (hit) {
+      const TriRec64 tr = vload_tri(P.sc.tris, h.slot);
+      hi.face = tr.face;
+      hi.p = f3{cur.o.x + h.t * cur.d.x, cur.o.y + h.t * cur.d.y, cur.o.z + h.t * cur.d.z};
+      hi.n = hit_normal(P.sc, tr, hi.p, hi.mat);
+    }
+    const f3 direct = calc_color<true, STATS, TRAV>(P, st, hi, cur.o, hit, &lds, wv, cnt);
+    if (depth == 0) {
+      h0 = h;
+      hit0 = hit;
+      face0 = hit ? hi.face : 0xFFFFFFFFu;
+      direct0 = direct;
+      if (hit && hi.mat != -1) st.ks = load_mat(P.sc.mats[hi.mat]).ks;  // traceRay :355-358
+      // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
+      Ray rr;
+      rr.d = reflect(normalized(cur.d), hi.n);
+      rr.o = offset(hi.p, rr.d, 0.001f);
+      rr.o2 = affv3(P.Minv, rr.o);
+      rr.d2 = normalized(m3v3(P.MS, rr.d));
+      setup_cull(rr);
+      if (STATS && hit) cnt[ST_TOTAL]++;
+      cur = rr;
+      act = hit;
+    } else if (hit) {
+      if (hi.mat != -1) st.ks = load_mat(P.sc.mats[hi.mat]).ks;
+      // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
+      refl = f3{clamp01(direct.x + 0.0f * st.ks.x), clamp01(direct.y + 0.0f * st.ks.y),
+                clamp01(direct.z + 0.0f * st.ks.z)};
+    }
+  }
+  if (!hit0) return f3{P.bg[0], P.bg[1], P.bg[2]};
+  return f3{clamp01(direct0.x + refl.x * st.ks.x), clamp01(direct0.y + refl.y * st.ks.y),
+            clamp01(direct0.z + refl.z * st.ks.z)};
+}
+
 #ifndef RT_FULL_WAVES_PER_EU
 #define RT_FULL_WAVES_PER_EU 8  // measured: 8 waves (64 VGPR + stack spill) beats 3 (150 VGPR) by 24% on C3 FULL
 #endif
@@ -1265,7 +1326,8 @@ void k_render_full(FrameParams P) {
 
   Hit h;
   uint32_t face0;
-  const f3 col = trace_full<STATS, TRAV>(P, r, active, lds, c.wv, cnt, h, face0);
+  const f3 col = RT_FULL_LOOP ? trace_full_loop<STATS, TRAV>(P, r, active, lds, c.wv, cnt, h, face0)
+                              : trace_full<STATS, TRAV>(P, r, active, lds, c.wv, cnt, h, face0);
   const bool hit0 = face0 != 0xFFFFFFFFu;
   if (active) {
     const size_t pix = (size_t)c.py * P.W + c.px;
