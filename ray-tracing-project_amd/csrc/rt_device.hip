@@ -1078,6 +1078,51 @@ void k_trace_primary(FrameParams P) {
   if (STATS) flush_stats(P, cnt, c.lane);
 }
 
+// Persistent-threads form of k_trace_primary (A/B variant bit 2048): one launch of as many one-wave
+// blocks as the device holds at 8 waves per SIMD; each wave repeatedly takes the next 8x8 work item
+// from its XCD's counter (XCD x owns items [x Q/8, (x+1) Q/8) of the shard's Q = 4 * tiles items, so
+// an XCD works through a contiguous band of tiles) and, once that range is exhausted, from the other
+// XCDs' counters in turn. The next item's atomic is issued before the current item is traced, so its
+// latency overlaps the traversal. Same per-pixel work and outputs as k_trace_primary.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
+void k_trace_primary_persistent(FrameParams P, uint32_t* queue, uint32_t max_steal) {
+  __shared__ WaveLds<TRAV_B2_LDS, false> lds;
+  const int lane = (int)(threadIdx.x & 63);
+  const uint32_t Q = 4u * (uint32_t)P.n_tiles_shard;
+  const uint32_t x0 = blockIdx.x & 7u;
+  uint32_t k = 0;  // counters visited so far (own XCD first)
+  auto take = [&](uint32_t x) -> uint32_t {
+    uint32_t i = 0;
+    if (lane == 0) i = atomicAdd(queue + x, 1u);
+    return uniform(i);
+  };
+  auto item_of = [&](uint32_t x, uint32_t i) -> uint32_t {  // global item or ~0u when x's range is done
+    const uint32_t lo = (uint32_t)(((uint64_t)Q * x) / 8), hi = (uint32_t)(((uint64_t)Q * (x + 1)) / 8);
+    return lo + i < hi ? lo + i : 0xFFFFFFFFu;
+  };
+  uint32_t cur = item_of(x0, take(x0));
+  for (;;) {
+    while (cur == 0xFFFFFFFFu && k < max_steal) {  // steal from the next XCD's range
+      k++;
+      const uint32_t x = (x0 + k) & 7u;
+      cur = item_of(x, take(x));
+    }
+    if (cur == 0xFFFFFFFFu) break;  // every range exhausted: all waves reach this exit
+    const uint32_t xk = (x0 + k) & 7u;
+    const uint32_t nxt_i = take(xk);  // the next item from the same counter, requested early
+    const int b = (int)(cur >> 2), wv = (int)(cur & 3);
+    const int tile = P.shard_index + b * P.shard_count;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int px = tx * 16 + (wv & 1) * 8 + (lane & 7), py = ty * 16 + (wv >> 1) * 8 + (lane >> 3);
+    const bool active = px < P.W && py < P.H;
+    const Ray r = primary_ray(P, px, py);
+    Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, active, h, lds, 0, nullptr);
+    if (active) P.hits[(size_t)py * P.W + px] = make_uint2(__float_as_uint(h.t), h.slot);
+    cur = item_of(xk, nxt_i);
+  }
+}
+
 // Two rays per lane (128-ray packets, one 16x8 pixel half-tile per wave): the per-node scalar work
 // (fetch, decision, stack) is shared by twice as many rays and each lane carries two independent
 // slab / triangle streams. Closest hit only (PRIMARY), LDS stack.
@@ -1843,7 +1888,7 @@ void device_release(rt_scene* s) {
     if (b) (void)hipFree(b);
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
-    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full};
+    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue};
     for (void* b : fb)
       if (b) (void)hipFree(b);
     if (f.stream) (void)hipStreamDestroy((hipStream_t)f.stream);
@@ -1934,8 +1979,9 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 // them), 4 = XCD-contiguous tile order, 512 / 1024 / 1536 = block runs of 4 / 16 / plain dispatch order
 // instead of the default 64-block runs per XCD, 16 = FULL as the stage pipeline (k_full_*) instead of one
 // kernel; with 16: 32 / 64 / 128 = per-lane traversal for the reflection rays / the shadow rays of
-// reflection hits / the shadow rays of primary hits. Default: binary nodes + LDS stack, FULL as one
-// kernel (k_render_full).
+// reflection hits / the shadow rays of primary hits; 256 = two rays per lane (PRIMARY), 2048 =
+// persistent-threads PRIMARY traversal with per-XCD work counters. Default: binary nodes + LDS stack,
+// FULL as one kernel (k_render_full).
 static int pick_trav(const FrameParams& P, int variant) {
   if (variant & 1) return TRAV_B2_VGPR;
   if ((variant & 2) && P.sc.n_nodes4 > 0) return TRAV_W4;
@@ -2135,6 +2181,16 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       if (stats) launch_trace<true>(P, grid, st, trav);
       else if ((variant & 256) && trav == TRAV_B2_LDS)
         hipLaunchKernelGGL(k_trace_primary_x2, dim3(2 * grid), dim3(64), 0, st, P);
+      else if ((variant & 2048) && trav == TRAV_B2_LDS && !P.wcount0) {
+        if (!slot.d_queue) HIPCHECK(hipMalloc((void**)&slot.d_queue, 8 * sizeof(uint32_t)));
+        HIPCHECK(hipMemsetAsync(slot.d_queue, 0, 8 * sizeof(uint32_t), st));
+        int cus = 0;
+        HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
+        const int waves = std::min(4 * grid, std::max(8, cus * 4 * RT_TRACE_WAVES_PER_EU));
+        // 4096: no stealing (each XCD's waves finish its own range; needs every XCD to get waves)
+        hipLaunchKernelGGL(k_trace_primary_persistent, dim3(std::max(waves, 8)), dim3(64), 0, st, P, slot.d_queue,
+                           (variant & 4096) ? 0u : 7u);
+      }
       else launch_trace<false>(P, grid, st, trav);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));

@@ -95,6 +95,7 @@ struct rt_scene {
     void* d_full = nullptr;  // FULL stage-pipeline hand-off buffers
     size_t full_pixels = 0;
     void* last_done = nullptr;  // event after this slot's latest frame (since the last synchronize)
+    uint32_t* d_queue = nullptr;  // persistent-threads variant: 8 per-XCD work counters
   };
   static constexpr int kMaxSlots = 4;
   FrameSlot slots[kMaxSlots];
