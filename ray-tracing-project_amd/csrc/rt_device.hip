@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -2041,13 +2042,16 @@ static void launch_full_pipeline(const FrameParams& P, int grid, hipStream_t st,
   else hipLaunchKernelGGL(k_full_final<false>, dim3(grid), dim3(256), 0, st, P);
 }
 
-static int g_variant = -1;  // RT_KERNEL_VARIANT, or rt_debug_set_variant()
+static std::atomic<int> g_variant{-1};  // RT_KERNEL_VARIANT, or rt_debug_set_variant()
 static int kernel_variant() {
-  if (g_variant < 0) {
+  int v = g_variant.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = getenv("RT_KERNEL_VARIANT");
-    g_variant = e ? atoi(e) : 0;
+    int want = e ? atoi(e) : 0;
+    want = want < 0 ? 0 : want;
+    if (g_variant.compare_exchange_strong(v, want)) v = want;  // v: the value another thread set
   }
-  return g_variant;
+  return v;
 }
 
 }  // namespace rt
@@ -2063,7 +2067,7 @@ static int check_device_scene(rt_scene* s) {
 
 extern "C" int rt_debug_set_variant(int32_t v) {
   const int prev = kernel_variant();
-  g_variant = v < 0 ? 0 : v;
+  g_variant.store(v < 0 ? 0 : v);
   return prev;
 }
 
