@@ -178,7 +178,7 @@ def main():
     ap.add_argument("--builder", choices=["sah", "lbvh"], default="sah",
                     help="BVH builder: host binned SAH (default) or the device LBVH (SURVEY f2)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
-                    help="frames that may overlap on the GPU (0 = library default, 3)")
+                    help="frames that may overlap on the GPU (0 = library default, 4)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,7 +222,7 @@ def main():
     sc = rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight,
                   builder=rt.RT_BUILDER_LBVH_GPU if a.builder == "lbvh" else rt.RT_BUILDER_SAH)
     info = sc.info()
-    info_fif = a.frames_in_flight or 3
+    info_fif = a.frames_in_flight or 4
     setup_s = time.perf_counter() - t0
     cam = rt.flycam(W, H, 0, 0, 20)
     mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY

@@ -99,7 +99,7 @@ typedef struct rt_scene_opts {
   int32_t leaf_size;      /* BVH leaf size bound (1..16), 0 = default (4 for SAH, 1 for the GPU LBVH) */
   rt_material default_material; /* Flyscene::ka/kd/ks/shininess defaults (flyscene.hpp:179-184) */
   float background[3];    /* Flyscene::BACKGROUND_COLOR (flyscene.hpp:175) */
-  int32_t frames_in_flight; /* rt_render_async frames that may execute concurrently (1..4, default 3):
+  int32_t frames_in_flight; /* rt_render_async frames that may execute concurrently (1..4, default 4):
                              * each in-flight frame has its own stream and frame buffers; frames stay
                              * independent and rt_frame_download returns the most recent one */
   int32_t builder;          /* RT_BUILDER_SAH (host binned SAH, default: fastest traversal) or

@@ -552,7 +552,7 @@ extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
   o->min_faces = 300;       // flyscene.hpp:168
   o->max_boxes = INT32_MAX; // flyscene.hpp:169
   o->leaf_size = 0;
-  o->frames_in_flight = 3;
+  o->frames_in_flight = 4;
   for (int k = 0; k < 3; k++) { o->default_material.ka[k] = 0.2f; o->background[k] = 0.9f; }
   o->default_material.kd[0] = 0.9f; o->default_material.kd[1] = 0.9f; o->default_material.kd[2] = 0.0f;
   o->default_material.shininess = 0.0f;
