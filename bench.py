@@ -164,7 +164,7 @@ def measured_traffic(W, H, n_faces, mode, kernel_ms):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tris", type=int, default=1_000_000)
     ap.add_argument("--frame", default=None, help="WxH (strong scaling); default 1080p per GPU (weak)")
