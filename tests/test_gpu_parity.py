@@ -189,7 +189,8 @@ def test_stats_counting_run(rt, soup):
 
 
 VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-pipeline": 16, "pipeline-lane-refl": 48,
-            "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256}
+            "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
+            "persistent-no-steal": 2048 | 4096}
 
 
 @pytest.mark.parametrize("name", sorted(VARIANTS))
@@ -215,7 +216,7 @@ def test_kernel_variants_render_identical_bits(rt, soup, name):
 
 
 def test_frames_in_flight_are_independent(rt, soup):
-    """Frames queued back to back overlap on the scene's frame slots (default 2 in flight, each with its
+    """Frames queued back to back overlap on the scene's frame slots (default 4 in flight, each with its
     own stream and buffers); every frame is still complete and independent: the downloaded last frame
     equals the same camera rendered alone, for 1, 2 and 4 slots, across frame-size changes."""
     _, osc = soup
