@@ -1357,11 +1357,19 @@ __device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r
             clamp01(direct0.z + refl.z * st.ks.z)};
 }
 
+// Occupancy of the FULL megakernel, by scene: 8 waves per SIMD (64 VGPR + a 272-B spill) for scenes
+// whose node + triangle records exceed the chip's aggregate L2 (the 1M soup: 8 waves beat 5 by 18% and
+// 3 by 24% -- the traversal waits on L2 misses and needs the waves), 5 waves (96 VGPR, 76 B spill) for
+// smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident, the spill traffic costs more).
 #ifndef RT_FULL_WAVES_PER_EU
-#define RT_FULL_WAVES_PER_EU 8  // measured: 8 waves (64 VGPR + stack spill) beats 3 (150 VGPR) by 24% on C3 FULL
+#define RT_FULL_WAVES_PER_EU 8
 #endif
-template <bool STATS, bool HITS, int TRAV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU)))
+#ifndef RT_FULL_WAVES_PER_EU_SMALL
+#define RT_FULL_WAVES_PER_EU_SMALL 5
+#endif
+constexpr size_t kFullSmallSceneBytes = 32u << 20;  // 8 XCDs x 4 MiB L2
+template <bool STATS, bool HITS, int TRAV, int WPE = RT_FULL_WAVES_PER_EU>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_render_full(FrameParams P) {
   __shared__ WaveLds<TRAV, STATS> lds;
   const PixelCoord c = pixel_coord(P);
@@ -1981,8 +1989,10 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 // instead of the default 64-block runs per XCD, 16 = FULL as the stage pipeline (k_full_*) instead of one
 // kernel; with 16: 32 / 64 / 128 = per-lane traversal for the reflection rays / the shadow rays of
 // reflection hits / the shadow rays of primary hits; 256 = two rays per lane (PRIMARY), 2048 =
-// persistent-threads PRIMARY traversal with per-XCD work counters. Default: binary nodes + LDS stack,
-// FULL as one kernel (k_render_full).
+// persistent-threads PRIMARY traversal with per-XCD work counters (4096: without stealing); 8192 /
+// 16384 = the FULL megakernel's 8-wave / small-scene (5-wave) build regardless of the scene size.
+// Default: binary nodes + LDS stack, FULL as one kernel (k_render_full) at the occupancy its scene
+// size selects.
 static int pick_trav(const FrameParams& P, int variant) {
   if (variant & 1) return TRAV_B2_VGPR;
   if ((variant & 2) && P.sc.n_nodes4 > 0) return TRAV_W4;
@@ -1996,8 +2006,10 @@ static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int tra
   else hipLaunchKernelGGL((k_trace_primary<STATS, TRAV_W4>), g, b, 0, st, P);
 }
 template <bool STATS, bool HITS>
-static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav) {
+static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav, bool small) {
   if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_VGPR>), dim3(grid), dim3(256), 0, st, P);
+  else if (trav == TRAV_B2_LDS && !STATS && small)
+    hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS, RT_FULL_WAVES_PER_EU_SMALL>), dim3(grid), dim3(256), 0, st, P);
   else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P);
   else hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_W4>), dim3(grid), dim3(256), 0, st, P);
 }
@@ -2201,8 +2213,11 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       if (hits) hipLaunchKernelGGL(k_shade_primary<true>, dim3(grid), dim3(256), 0, st, P);
       else hipLaunchKernelGGL(k_shade_primary<false>, dim3(grid), dim3(256), 0, st, P);
     } else if (!(variant & 16)) {  // FULL as one kernel (default); 16 = the stage pipeline
-      if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav); else launch_full<true, false>(P, grid, st, trav); }
-      else { if (hits) launch_full<false, true>(P, grid, st, trav); else launch_full<false, false>(P, grid, st, trav); }
+      // occupancy by scene size (k_render_full); variant bits 8192 / 16384 force the 8-wave / small build
+      const size_t rec_bytes = (s->hs.nodes.size() + s->hs.tris.size()) * 64;
+      const bool small = (variant & 16384) || (!(variant & 8192) && rec_bytes <= kFullSmallSceneBytes);
+      if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav, small); else launch_full<true, false>(P, grid, st, trav, small); }
+      else { if (hits) launch_full<false, true>(P, grid, st, trav, small); else launch_full<false, false>(P, grid, st, trav, small); }
       HIPCHECK(hipEventRecord(ev_m, st));
     } else {
       if (stats) launch_full_pipeline<true>(P, grid, st, trav, variant, hits, ev_m);
