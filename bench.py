@@ -143,7 +143,7 @@ def make_reducer(dist, dev):
     return reduce
 
 
-def measured_traffic(W, H, n_faces, mode, kernel_ms):
+def measured_traffic(W, H, n_faces, mode, kernel_ms, kernel):
     """HBM traffic of the same kernel on the same workload from the committed rocprofv3 PMC summary
     (profiles/pmc_latest.json, tools/profile.sh + tools/summarize_profile.py): 2*FETCH_SIZE + WRITE_SIZE
     bytes per launch (gfx950 correction), expressed as GB/s over this run's average launch time."""
@@ -153,6 +153,8 @@ def measured_traffic(W, H, n_faces, mode, kernel_ms):
     d = json.load(open(p))
     cfg = d.get("bench_line_under_trace", {}).get("config", {})
     if cfg.get("frame") != f"{W}x{H}" or cfg.get("triangles") != n_faces or cfg.get("mode") != mode:
+        return None, None
+    if not str(d.get("kernel", "")).startswith(kernel + "<"):  # profiled with another kernel form
         return None, None
     b = d.get("hbm_bytes_per_launch")
     if not b:
@@ -262,24 +264,27 @@ def main():
         n_node = stats["node_visits"] / rays
         n_tri = stats["tri_tests"] / rays
         hit = stats["hits"] / rays
-        # B = 64 N_node + 40 N_tri + 92 hit + 12 per ray. The dominant kernel is the
-        # traversal kernel (PRIMARY: k_trace_primary), whose share of B is 64 N_node + 40 N_tri plus
-        # its 8-B hit-record store; the shading kernel carries the 92*hit + 12.
+        # B = 64 N_node + 40 N_tri + 92 hit + 12 per ray. PRIMARY runs as one kernel
+        # (k_primary_fused: traversal + shading, so its share is the whole B); with RT_KERNEL_VARIANT bit
+        # 32768 it runs as k_trace_primary (64 N_node + 40 N_tri + its 8-B hit record) + k_shade_primary.
+        # FULL: k_render_full carries B (its secondary rays on top are not counted).
+        split = mode == rt.RT_MODE_PRIMARY and (int(os.environ.get("RT_KERNEL_VARIANT", "0") or 0) & (32768 | 256 | 2048))
         b_trace = 64 * n_node + 40 * n_tri + 8
         b_ray = 64 * n_node + 40 * n_tri + 92 * hit + 12
+        b_kern = b_trace if split else b_ray
         kern_ms = trace_ms_avg if mode == rt.RT_MODE_PRIMARY else kernel_ms_avg
-        achieved = (b_trace if mode == rt.RT_MODE_PRIMARY else b_ray) * st["primary_rays"] / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_note = measured_traffic(W, H, info["n_faces"], a.mode, kern_ms)
+        achieved = b_kern * st["primary_rays"] / (kern_ms * 1e-3) / 1e9
+        kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
+        traffic, traffic_note = measured_traffic(W, H, info["n_faces"], a.mode, kern_ms, kname)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic, "traffic_source": traffic_note,
-                "kernel": "k_trace_primary" if mode == rt.RT_MODE_PRIMARY else "k_render_full",
-                "kernel_ms": round(kern_ms, 4), "bytes_per_ray_kernel": round(b_trace, 1),
+                "kernel": kname,
+                "kernel_ms": round(kern_ms, 4), "bytes_per_ray_kernel": round(b_kern, 1),
                 "bytes_per_ray_path": round(b_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
                 "hit": round(hit, 4),
                 "path_achieved_GBps": round(b_ray * st["primary_rays"] / (kernel_ms_avg * 1e-3) / 1e9, 1),
                 # the same bytes over the wall-clock interval per frame (frames overlap in flight)
-                "achieved_throughput_GBps": round((b_trace if mode == rt.RT_MODE_PRIMARY else b_ray) * st["primary_rays"]
-                                                  / (elapsed / a.steps) / 1e9, 1),
+                "achieved_throughput_GBps": round(b_kern * st["primary_rays"] / (elapsed / a.steps) / 1e9, 1),
                 "wave_fetch_bytes_per_ray": round((64 * stats["wave_node_fetches"] + 64 * stats["wave_tri_fetches"]) / rays, 2)}
 
     e2e = None

@@ -17,8 +17,14 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_trace_primary<false, 1>"):
+def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    if kernel is None:  # the bench line's dominant kernel, non-counting instantiation
+        try:
+            bl = json.loads(open(os.path.join(prof, "trace_bench.json")).read().strip().splitlines()[-1])
+            kernel = bl["roofline"]["kernel"] + "<false"
+        except Exception:
+            kernel = "k_primary_fused<false"
     stats_src = os.path.join(prof, "trace", "run_kernel_stats.csv")
     shutil.copy(stats_src, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     avg_ns = None
