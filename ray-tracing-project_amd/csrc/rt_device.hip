@@ -203,10 +203,8 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
   if (!(tr.box & kSafeNormalBit)) {  // uniform branch: only faces the host could not certify
     const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
     const float area = norm(cross(e0, neg(e2))) / 2;
-    const uint32_t* fs = P.fshade + 4 * (size_t)tr.face;
-    const f3 n0 = ld3(P.vnorm + 4 * (size_t)fs[0]);
-    const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs[1]);
-    const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs[2]);
+    const float* fs = P.fshade + 12 * (size_t)tr.face;
+    const f3 n0 = ld3(fs), n1 = ld3(fs + 4), n2 = ld3(fs + 8);
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
     cand &= fmask<kFcmpUNE>(norm(nn), 0.0f);
   }
@@ -703,10 +701,8 @@ __device__ __forceinline__ bool accept_lane(const DevScene& P, const TriRec64& t
   if (!(tr.box & kSafeNormalBit)) {
     const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
     const float area = norm(cross(e0, neg(e2))) / 2;
-    const uint4 fs = *reinterpret_cast<const uint4*>(P.fshade + 4 * (size_t)tr.face);
-    const f3 n0 = ld3(P.vnorm + 4 * (size_t)fs.x);
-    const f3 n1 = ld3(P.vnorm + 4 * (size_t)fs.y);
-    const f3 n2 = ld3(P.vnorm + 4 * (size_t)fs.z);
+    const float* fs = P.fshade + 12 * (size_t)tr.face;
+    const f3 n0 = ld3(fs), n1 = ld3(fs + 4), n2 = ld3(fs + 8);
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
     if (!(norm(nn) != 0)) return false;
   }
@@ -888,20 +884,20 @@ __device__ __forceinline__ MatState load_mat(const DevMat& m) {
   return MatState{f3{m.ka[0], m.ka[1], m.ka[2]}, f3{m.kd[0], m.kd[1], m.kd[2]}, f3{m.ks[0], m.ks[1], m.ks[2]}, m.ns};
 }
 
-// interpolateNormal (flyscene.cpp:572-600) for the hit triangle of this lane (per-lane gathers)
+// interpolateNormal (flyscene.cpp:572-600) for the hit triangle of this lane: one contiguous 48-B
+// gather of the face's shading record (its three unit vertex normals + material)
 __device__ __forceinline__ f3 hit_normal(const DevScene& P, const TriRec64& tr, f3 p, int32_t& mat) {
   const f3 n{tr.nx, tr.ny, tr.nz};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  const uint4 fs = *reinterpret_cast<const uint4*>(P.fshade + 4 * (size_t)tr.face);
-  mat = (int32_t)fs.w;
+  const float4* fs = reinterpret_cast<const float4*>(P.fshade + 12 * (size_t)tr.face);
+  const float4 n0 = fs[0];
+  mat = __float_as_int(n0.w);
   if (dot(n, a0) < 0 || dot(n, a1) < 0 || dot(n, a2) < 0) return f3{0.0f, 0.0f, 0.0f};
   const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
   const float area = norm(cross(e0, neg(e2))) / 2;
-  const float4 n0 = *reinterpret_cast<const float4*>(P.vnorm + 4 * (size_t)fs.x);
-  const float4 n1 = *reinterpret_cast<const float4*>(P.vnorm + 4 * (size_t)fs.y);
-  const float4 n2 = *reinterpret_cast<const float4*>(P.vnorm + 4 * (size_t)fs.z);
+  const float4 n1 = fs[1], n2 = fs[2];
   return blend_normal(f3{n0.x, n0.y, n0.z}, f3{n1.x, n1.y, n1.z}, f3{n2.x, n2.y, n2.z}, area0, area1, area2, area);
 }
 
@@ -1881,19 +1877,21 @@ int device_upload(rt_scene* s) {
     if (nt) HIPCHECK(hipMemcpy(s->d_tris, hs.tris.data(), nt * 64, hipMemcpyHostToDevice));
   }
   if ((rc = dalloc_copy(&s->d_nodes4, hs.nodes4.data(), hs.nodes4.size() * sizeof(Node4Q), tot))) return rc;
-  std::vector<uint32_t> fshade(4 * (size_t)hs.nf);
-  for (int32_t f = 0; f < hs.nf; f++) {
-    fshade[4 * f + 0] = hs.fidx[3 * f + 0];
-    fshade[4 * f + 1] = hs.fidx[3 * f + 1];
-    fshade[4 * f + 2] = hs.fidx[3 * f + 2];
-    fshade[4 * f + 3] = (uint32_t)hs.fmat[f];
+  {
+    // per-face shading record (float4 x 3): the unit normals of the face's three vertices (Mesh normals
+    // as interpolateNormal normalises them, flyscene.cpp:599) and the material id in the first .w
+    std::vector<float> fsh(12 * (size_t)hs.nf, 0.0f);
+    for (int32_t f = 0; f < hs.nf; f++) {
+      float* r = fsh.data() + 12 * (size_t)f;
+      for (int k = 0; k < 3; k++) {
+        const f3 n = hs.vnn[hs.fidx[3 * f + k]];
+        r[4 * k] = n.x; r[4 * k + 1] = n.y; r[4 * k + 2] = n.z;
+      }
+      const int32_t m = hs.fmat[f];
+      memcpy(&r[3], &m, 4);
+    }
+    if ((rc = dalloc_copy(&s->d_fshade, fsh.data(), fsh.size() * 4, tot))) return rc;
   }
-  if ((rc = dalloc_copy(&s->d_fshade, fshade.data(), fshade.size() * 4, tot))) return rc;
-  std::vector<float> vn(4 * (size_t)hs.nv);
-  for (int32_t i = 0; i < hs.nv; i++) {
-    vn[4 * i] = hs.vnn[i].x; vn[4 * i + 1] = hs.vnn[i].y; vn[4 * i + 2] = hs.vnn[i].z; vn[4 * i + 3] = 0.0f;
-  }
-  if ((rc = dalloc_copy(&s->d_vnorm, vn.data(), vn.size() * 4, tot))) return rc;
   std::vector<float> rb(8 * hs.boxes.size());
   for (size_t b = 0; b < hs.boxes.size(); b++) {
     for (int k = 0; k < 3; k++) { rb[8 * b + k] = hs.boxes[b].low[k]; rb[8 * b + 4 + k] = hs.boxes[b].high[k]; }
@@ -1916,7 +1914,7 @@ void device_release(rt_scene* s) {
   (void)hipSetDevice(s->device);
   for (int k = 0; k < s->n_slots; k++)
     if (s->slots[k].stream) (void)hipStreamSynchronize((hipStream_t)s->slots[k].stream);
-  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_vnorm, s->d_refbox, s->d_mats, s->d_stats};  // d_tris: inside d_nodes
+  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_refbox, s->d_mats, s->d_stats};  // d_tris: inside d_nodes
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (int k = 0; k < s->n_slots; k++) {
@@ -1938,7 +1936,6 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.nodes = s->d_nodes;
   P.sc.tris = s->d_tris;
   P.sc.fshade = s->d_fshade;
-  P.sc.vnorm = s->d_vnorm;
   P.sc.refbox = s->d_refbox;
   P.sc.mats = s->d_mats;
   P.sc.root = hs.root;

@@ -5,8 +5,8 @@
 //                                  (one 64-B record = one s_load_dwordx16 per wave per visit)
 //   tris     TriRec64[n_faces]     exact-test data in BVH leaf order: unit face normal, plane distance,
 //                                  world vertices, reference rank / face id / reference box id
-//   fshade   uint4[n_faces]        per face id: vertex ids + material (touched only by the final hit)
-//   vnorm    float4[n_vertices]    normalised vertex normals (interpolateNormal, flyscene.cpp:599)
+//   fshade   float4[3*n_faces]     per face id: the three normalised vertex normals (interpolateNormal,
+//                                  flyscene.cpp:599) + material id; read by the final hit (one 48-B gather)
 //   refbox   float4[2*n_boxes]     reference flat boxes, object space (BoundingBox::low/high)
 //   mats     float4[3*n_mats]      ka|Ns, kd|-, ks|- per material
 // Frame buffers: rgb float[H][W][3]; optional face int32[H][W], t float[H][W]; stats counters.
@@ -93,8 +93,7 @@ struct DevScene {
   uint32_t root4;
   int32_t n_nodes4;
   const TriRec64* tris;
-  const uint32_t* fshade;  // uint4 per face
-  const float* vnorm;      // float4 per vertex
+  const float* fshade;     // float4 x 3 per face: unit vertex normals (n0 .w = material id bits)
   const float* refbox;     // 2 float4 per box
   const DevMat* mats;
   uint32_t root;           // root handle; n_nodes == 0 -> empty scene

@@ -76,8 +76,7 @@ struct rt_scene {
   rt::Node64* d_nodes = nullptr;
   rt::Node4Q* d_nodes4 = nullptr;
   rt::TriRec64* d_tris = nullptr;
-  uint32_t* d_fshade = nullptr;
-  float* d_vnorm = nullptr;
+  float* d_fshade = nullptr;  // per-face shading record: three unit vertex normals + material (float4 x 3)
   float* d_refbox = nullptr;
   rt::DevMat* d_mats = nullptr;
   unsigned long long* d_stats = nullptr;
