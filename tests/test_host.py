@@ -261,3 +261,20 @@ def test_directional_light_is_screen_centre(rt, orc):
         diff = np.array(v, np.float32) - np.array(o, np.float32)
         n = np.float32(np.sqrt(np.float32(diff[0] * diff[0] + (diff[1] * diff[1] + diff[2] * diff[2]))))
         assert np.array_equal((diff / n).astype(np.float32), np.array(d, np.float32))
+
+
+def test_face_limit_rejected_before_reading(rt):
+    """Scenes beyond the 32-bit record addressing limit (2^25 - 1 faces, rt_api.h) are refused up front,
+    before any array is read (the descriptor's pointers still describe the 12-face cube)."""
+    import ctypes as C
+    m = rt.Mesh.load_obj(scene_path("cube.obj"))
+    d = m.desc()
+    o = rt.SceneOpts()
+    rt.lib().rt_scene_opts_default(C.byref(o))
+    o.device = rt.RT_DEVICE_NONE
+    h = C.c_void_p()
+    for n in (1 << 25, 1 << 26):
+        d.n_faces = n
+        rc = rt.lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(h))
+        assert rc != 0 and not h.value, n
+        assert "face limit" in rt.lib().rt_last_error().decode()
