@@ -865,6 +865,9 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #ifndef RT_FULL_OCT
 #define RT_FULL_OCT 0
 #endif
+#ifndef RT_FULL_OCT_PRIMARY
+#define RT_FULL_OCT_PRIMARY 1
+#endif
 template <bool ANY, bool STATS, int TRAV>
 __device__ __forceinline__ void trace_full_ray(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                                WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
@@ -1257,7 +1260,9 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
                                          uint32_t* cnt, Hit& h, uint32_t& face0) {
   h = Hit{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
-  trace_full_ray<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
+  // the primary packet is coherent: octant-specialised loops for it alone (A/B knob RT_FULL_OCT_PRIMARY)
+  if (RT_FULL_OCT_PRIMARY) trace_oct<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
+  else trace_full_ray<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
   const bool hit0 = active && h.t != INFINITY;
   if (STATS && hit0) cnt[ST_HITS]++;
 
