@@ -296,7 +296,8 @@ const char* rt_last_error(void); /* thread-local */
 
 /* Verification hooks (tests only; never used by the render path): evaluate the Eigen-order float
  * primitives of rt_math.h on the host (rt_debug_math_host) or in a gfx950 kernel
- * (rt_debug_math_device) for n known-answer cases of op (tests/golden/eigen_kat.bin). */
+ * (rt_debug_math_device) for n known-answer cases of op (tests/golden/eigen_kat.bin; op 17 = the
+ * specular term's pow, in {x, y} -> out {pow}, checked against the host C library). */
 int rt_debug_math_host(int32_t op, int32_t n, const float* in, float* out);
 int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
 

@@ -912,8 +912,6 @@ __device__ __forceinline__ TriRec64 vload_tri(const TriRec64* base, uint32_t i) 
   return r;
 }
 
-// std::pow(float,float) -> powf: evaluated in fp64 then rounded (matches a correctly rounded powf)
-__device__ __forceinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }
 
 // calculateColor's light direction (flyscene.cpp:607-611): point light -(P - pos).normalized(), or a
 // directional light's stored vector as is
@@ -2535,9 +2533,9 @@ extern "C" int rt_trace_color(rt_scene* s, int32_t n, const float* o, const floa
 }
 
 extern "C" int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out) {
-  static const int in_len[] = {6, 3, 6, 12, 19, 20, 9, 16, 4, 6, 6, 6, 6, 13, 3, 16, 24};
-  static const int out_len[] = {1, 3, 3, 3, 3, 4, 9, 16, 16, 3, 3, 3, 3, 3, 1, 3, 3};
-  if (op < 0 || op > 16 || n <= 0 || !in || !out) { set_error("rt_debug_math_device: bad arguments"); return RT_ERR_INVALID; }
+  static const int in_len[] = {6, 3, 6, 12, 19, 20, 9, 16, 4, 6, 6, 6, 6, 13, 3, 16, 24, 2};
+  static const int out_len[] = {1, 3, 3, 3, 3, 4, 9, 16, 16, 3, 3, 3, 3, 3, 1, 3, 3, 1};
+  if (op < 0 || op > 17 || n <= 0 || !in || !out) { set_error("rt_debug_math_device: bad arguments"); return RT_ERR_INVALID; }
   if (rt_device_count() == 0) { set_error("no HIP device"); return RT_ERR_NO_DEVICE; }
   float *di = nullptr, *dout = nullptr;
   const size_t ib = (size_t)n * in_len[op] * 4, ob = (size_t)n * out_len[op] * 4;

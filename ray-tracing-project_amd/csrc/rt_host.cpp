@@ -1384,9 +1384,9 @@ extern "C" int rt_scene_ref_boxes(const rt_scene* s, float* bounds6, int32_t* co
 #include "rt_kat.h"
 
 extern "C" int rt_debug_math_host(int32_t op, int32_t n, const float* in, float* out) {
-  static const int in_len[] = {6, 3, 6, 12, 19, 20, 9, 16, 4, 6, 6, 6, 6, 13, 3, 16, 24};
-  static const int out_len[] = {1, 3, 3, 3, 3, 4, 9, 16, 16, 3, 3, 3, 3, 3, 1, 3, 3};
-  if (op < 0 || op > 16 || n < 0 || !in || !out) { rt::set_error("rt_debug_math_host: bad op"); return RT_ERR_INVALID; }
+  static const int in_len[] = {6, 3, 6, 12, 19, 20, 9, 16, 4, 6, 6, 6, 6, 13, 3, 16, 24, 2};
+  static const int out_len[] = {1, 3, 3, 3, 3, 4, 9, 16, 16, 3, 3, 3, 3, 3, 1, 3, 3, 1};
+  if (op < 0 || op > 17 || n < 0 || !in || !out) { rt::set_error("rt_debug_math_host: bad op"); return RT_ERR_INVALID; }
   for (int32_t k = 0; k < n; k++)
     if (rt::debug_math_case(op, in + (size_t)k * in_len[op], out + (size_t)k * out_len[op])) return RT_ERR_INVALID;
   return RT_OK;

@@ -53,6 +53,7 @@ RT_HD int debug_math_case(int op, const float* a, float* o) {
       put(affv3(vinv, nc));
       return 0;
     }
+    case 17: o[0] = pow_ref(a[0], a[1]); return 0;  // calcSingleColor's std::pow (flyscene.cpp:562)
     default: return -1;
   }
 }

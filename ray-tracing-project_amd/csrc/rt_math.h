@@ -18,6 +18,11 @@
 #else
 #define RT_HD inline
 #endif
+#if defined(__HIPCC__) || defined(__HIP__)
+#define RT_HD_NOINLINE __host__ __device__ __attribute__((noinline)) inline
+#else
+#define RT_HD_NOINLINE __attribute__((noinline)) inline
+#endif
 
 namespace rt {
 
@@ -134,6 +139,32 @@ RT_HD f3 blend_normal(f3 n0, f3 n1, f3 n2, float area0, float area1, float area2
   return normalized(f3{(n0.x * area1 / area + n1.x * area2 / area) + n2.x * area0 / area,
                        (n0.y * area1 / area + n1.y * area2 / area) + n2.y * area0 / area,
                        (n0.z * area1 / area + n1.z * area2 / area) + n2.z * area0 / area});
+}
+
+// std::pow(float,float) -> powf (flyscene.cpp:562), evaluated in fp64 and rounded once to float.
+// Integer exponents 0..1023 (every material of the configured scenes: MTL Ns is an integer there) take
+// binary exponentiation in fp64: at most 20 products, each rounded to 2^-53, so the fp64 value is within
+// ~2^-48 relative of x^n and its rounding to float is the correctly rounded x^n except within that distance
+// of a float rounding midpoint -- the same exposure as the fp64 library pow. Other exponents call the
+// library pow out of line: inlined into a kernel, its fp64 polynomial constants are hoisted into registers
+// over the light loop and spilled (112 B per lane of scratch in k_primary_fused, 76-272 B in the FULL
+// megakernel builds).
+#ifndef RT_POW_INT
+#define RT_POW_INT 1
+#endif
+RT_HD_NOINLINE double pow_generic(double x, double y) { return pow(x, y); }
+RT_HD float pow_ref(float x, float y) {
+  if (RT_POW_INT && y >= 0.0f && y < 1024.0f && y == truncf(y)) {
+    uint32_t n = (uint32_t)y;
+    double b = (double)x, r = 1.0;
+    while (n != 0u) {
+      if (n & 1u) r *= b;
+      n >>= 1;
+      if (n != 0u) b *= b;
+    }
+    return (float)r;
+  }
+  return (float)pow_generic((double)x, (double)y);
 }
 
 }  // namespace rt

@@ -45,6 +45,21 @@ def test_device_math_matches_eigen(rt, sec):
     assert bad.sum() == 0, f"op {op}: {bad.sum()} of {n} cases differ on the device"
 
 
+def test_device_pow_matches_host(rt):
+    """op 17 in a gfx950 kernel: the integer-exponent path is bit-identical to the host's; other exponents
+    go to the device libm pow (fp64), within 1 ulp of the host C library's."""
+    from test_host import pairs, pow_cases, ulp_diff
+    xs, ints, frac = pow_cases()
+    for ys, exact in ((ints, True), (frac, False)):
+        inp = pairs(xs, ys)
+        dev = rt.debug_math(17, inp.reshape(-1), len(inp), 1, device=True).reshape(-1)
+        host = rt.debug_math(17, inp.reshape(-1), len(inp), 1, device=False).reshape(-1)
+        if exact:
+            assert same_bits(dev, host).all(), f"{int((~same_bits(dev, host)).sum())} cases differ"
+        else:
+            assert ulp_diff(dev, host).max() <= 1
+
+
 def golden_keys():
     g = np.load(os.path.join(GOLDEN, "images.npz"))
     return sorted({k.rsplit("_", 1)[0] for k in g.files})

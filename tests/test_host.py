@@ -71,6 +71,43 @@ def test_host_math_matches_eigen(rt, sec):
     assert bad.sum() == 0, f"op {op}: {bad.sum()} cases differ"
 
 
+def pow_cases(seed=7, n=20000):
+    """Inputs of op 17 (calcSingleColor's std::pow, flyscene.cpp:562): specular dots in [-1, 1] plus
+    special values, against integer exponents (the fast path) and non-integer / out-of-range ones."""
+    rng = np.random.default_rng(seed)
+    xs = np.concatenate([rng.uniform(-1, 1, n), rng.uniform(0.9, 1.0, n), rng.uniform(-4, 4, n // 4),
+                         [0.0, -0.0, 1.0, -1.0, 1e-30, -1e-30, 3e38, np.inf, -np.inf, np.nan, 1e-45]]).astype(np.float32)
+    ints = np.array([0, 1, 2, 3, 5, 16, 32, 100, 1000, 1023], np.float32)
+    frac = np.array([0.5, 1.5, 10.25, 32.5, 1024, 2000, -1, -2.5], np.float32)
+    return xs, ints, frac
+
+
+def pairs(xs, ys):
+    return np.stack(np.broadcast_arrays(xs[:, None], ys[None, :]), -1).reshape(-1, 2).astype(np.float32)
+
+
+def ulp_diff(a, b):
+    ai, bi = a.view(np.int32).astype(np.int64), b.view(np.int32).astype(np.int64)
+    ai = np.where(ai < 0, -(ai & 0x7FFFFFFF), ai)
+    bi = np.where(bi < 0, -(bi & 0x7FFFFFFF), bi)
+    d = np.abs(ai - bi)
+    return np.where(np.isnan(a) & np.isnan(b), 0, d)
+
+
+def test_host_pow_integer_fast_path(rt):
+    """op 17 on the host: integer exponents use fp64 binary exponentiation; the float result must be the
+    correctly rounded x^n (fp64 pow rounded once) and within 1 ulp of the reference's glibc powf."""
+    xs, ints, frac = pow_cases()
+    for ys in (ints, frac):
+        inp = pairs(xs, ys)
+        got = rt.debug_math(17, inp.reshape(-1), len(inp), 1, device=False).reshape(-1)
+        with np.errstate(all="ignore"):
+            cr = np.power(inp[:, 0].astype(np.float64), inp[:, 1].astype(np.float64)).astype(np.float32)
+            pf = np.power(inp[:, 0], inp[:, 1])  # float32 power: the C library's powf
+        assert same_bits(got, cr).all(), f"{int((~same_bits(got, cr)).sum())} cases differ from fp64 pow"
+        assert ulp_diff(got, pf).max() <= 1
+
+
 @pytest.mark.parametrize("name", ["cube", "dodgeColorTest", "bunny"])
 def test_reference_boxes_match_oracle(rt, orc, name):
     sc = rt.Scene(rt.Mesh.load_obj(scene_path(name + ".obj")), device=rt.RT_DEVICE_NONE)
