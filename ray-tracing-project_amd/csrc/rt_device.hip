@@ -271,14 +271,19 @@ struct WaveStack {
 // code); this loop serves the counting run and the VGPR-stack A/B variant.
 // Knobs (A/B builds; results are identical either way):
 //   RT_ORDER_BITS       octant-specialised loops take the near child from the node's precomputed order
-//                       bit for the wave's octant (Node64::pad0, split-axis rule) instead of a lane vote
+//                       bit for the wave's octant (split-axis rule, octant_order() in rt_host.cpp)
+//                       instead of a lane-majority vote: 3 fewer SALU and one fewer v_cmp per node step
+//                       (default 1; C3 +3.7% at 4 frames in flight, bunny +2.6%; 0 = the vote)
 //   RT_EXPERIMENT_SALU  timing experiment: N extra independent SALU per node step
 //   RT_EXPERIMENT_VALU  timing experiment: N extra independent VALU per node step
 #ifndef RT_ORDER_BITS
-#define RT_ORDER_BITS 0
+#define RT_ORDER_BITS 1
 #endif
 #ifndef RT_FAST_LOOP
 #define RT_FAST_LOOP 1
+#endif
+#ifndef RT_VADDR_PUSH  // 1: the wave stack's push address is scaled by a VALU op instead of an SALU op
+#define RT_VADDR_PUSH 0
 #endif
 #ifndef RT_EXPERIMENT_SALU
 #define RT_EXPERIMENT_SALU 0
@@ -287,14 +292,25 @@ struct WaveStack {
 #define RT_EXPERIMENT_VALU 0
 #endif
 // RT_PREFETCH: the fast loop prefetches both children's records into the scalar cache (Node64::pad0/1
-// then hold prefetch offsets instead of the order bits)
+// then hold prefetch offsets, with the order bits in their low bits)
 #ifndef RT_PREFETCH
 #define RT_PREFETCH 1
 #endif
 #ifndef RT_PREFETCH_PADLOAD  // 1: offsets re-loaded inside the node-load asm (0: tie-ordered separate asm, measured ±0.5%)
 #define RT_PREFETCH_PADLOAD 1
 #endif
-static_assert(!(RT_PREFETCH && RT_ORDER_BITS), "RT_PREFETCH reuses Node64::pad0 (the order bits)");
+// With RT_PREFETCH, Node64::pad0 / pad1 hold the children's record offsets (multiples of 64), so the
+// eight octant order bits travel in their low bits: octants 0-5 in pad0 bits 0-5, octants 6-7 in pad1
+// bits 0-1. A scalar load ignores the two low offset bits and the rest stays inside the 64-B record,
+// so the prefetch still touches the child's cache line.
+template <int OCT>
+__device__ __forceinline__ uint32_t order_word(const Node64& nd) {
+  return RT_PREFETCH ? (OCT < 6 ? nd.pad0 : nd.pad1) : nd.pad0;
+}
+template <int OCT>
+constexpr int order_bit() {
+  return RT_PREFETCH ? (OCT < 6 ? OCT : OCT - 6) : (OCT & 7);
+}
 #define RT_STR2(x) #x
 #define RT_STR(x) RT_STR2(x)
 template <bool ANY, bool STATS, bool STACK_LDS, int OCT = -1>
@@ -344,7 +360,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       bool first0;
       if (RT_ORDER_BITS && OCT >= 0) {
         // the node's order bit for this octant, overridden when only one child is needed
-        const bool pref1 = (nd.pad0 >> (OCT & 7)) & 1u;
+        const bool pref1 = (order_word<OCT>(nd) >> order_bit<OCT>()) & 1u;
         first0 = m1 == 0 || (m0 != 0 && !pref1);
       } else {
         // near child first by lane majority: each lane that needs a child votes for the one it enters
@@ -452,7 +468,14 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
       // decision block values it keeps in VGPRs; readfirstlane folds away on SGPR values)
       sp = (int)uniform((uint32_t)sp);
       const uint32_t c0 = uniform(nd.child0), c1 = uniform(nd.child1);
+#if RT_VADDR_PUSH
+      // the push address scaled in a VALU op (the scalar unit is the loop's tighter resource)
+      uint32_t vsp = (uint32_t)sp;
+      asm("" : "+v"(vsp));  // the depth as a VGPR operand: the shift below becomes a VALU op
+      uint32_t* const slot = lds_stack + vsp;
+#else
       uint32_t* const slot = lds_stack + sp;
+#endif
       if (RT_ORDER_BITS && OCT >= 0) {
         // near child from the node's order bit for this octant (Node64::pad0), overridden when only
         // one child is needed
@@ -469,8 +492,8 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
             "s_or_b64 %[tt], %[m0], %[m1]\n\t"
             "s_cselect_b32 %[nxt], %[nxt], -1"
             : [nxt] "=&s"(nxt), [far] "=&s"(far), [sp] "+s"(sp), [ta] "=&s"(ta), [tt] "=&s"(tt)
-            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [bits] "s"(uniform(nd.pad0)),
-              [oct] "i"(OCT & 7)
+            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [bits] "s"(uniform(order_word<OCT>(nd))),
+              [oct] "i"(order_bit<OCT>())
             : "scc");
         (void)tb;
         *slot = far;
@@ -1873,7 +1896,11 @@ int device_upload(rt_scene* s) {
       auto pf = [&](uint32_t c) -> uint32_t {
         return (uint32_t)(64 * (is_leaf(c) ? nn + leaf_first(c) : (size_t)c));
       };
-      for (Node64& nd : nodes) { nd.pad0 = pf(nd.child0); nd.pad1 = pf(nd.child1); }
+      for (Node64& nd : nodes) {
+        const uint32_t order = nd.pad0;  // octant_order() (rt_host.cpp), moved into the low offset bits
+        nd.pad0 = pf(nd.child0) | (order & 0x3Fu);
+        nd.pad1 = pf(nd.child1) | ((order >> 6) & 0x3u);
+      }
     }
     if (nn) HIPCHECK(hipMemcpy(s->d_nodes, nodes.data(), nn * 64, hipMemcpyHostToDevice));
     s->d_tris = reinterpret_cast<TriRec64*>(s->d_nodes + nn);
