@@ -64,15 +64,23 @@ __device__ __forceinline__ T sload64(const T* base, uint32_t i) {
   __builtin_memcpy(&r, &v, 64);
   return r;
 }
-__device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t i) { return sload64(base, i); }
+// Interior node handles on the device are byte offsets of the node record (RT_BYTE_HANDLES, set by
+// device_upload: index * 64, < 2^31 below kMaxFaces), so a node fetch needs no shift per step; leaf
+// handles keep the (first triangle, count) form. 0 = record indices (A/B).
+#ifndef RT_BYTE_HANDLES
+#define RT_BYTE_HANDLES 1
+#endif
+__device__ __forceinline__ uint32_t node_index(uint32_t h) { return RT_BYTE_HANDLES ? h >> 6 : h; }
+__device__ __forceinline__ uint32_t node_offset(uint32_t h) { return RT_BYTE_HANDLES ? h : h * 64u; }
+__device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t h) { return sload64(base, node_index(h)); }
 // The same node fetch, then a prefetch of both children's records into the scalar cache, issued the
 // moment the node has arrived so that it overlaps this node's box tests: one dword each pulls in the
 // 64-B line. pad0 / pad1 (loaded alongside, same line) are the byte offsets from the nodes base of
 // child 0 / 1's node record or, for a leaf child, of its first triangle record (device_upload).
 // pf0 / pf1 receive the prefetched dwords: the caller keeps them live until an s_waitcnt
 // lgkmcnt(0) has retired the loads (the hardware writes them whenever the data returns).
-__device__ __forceinline__ Node64 sload_node_pf(const Node64* base, uint32_t i, uint32_t& pf0, uint32_t& pf1) {
-  const uint32_t off = __builtin_amdgcn_readfirstlane(i) * 64u;
+__device__ __forceinline__ Node64 sload_node_pf(const Node64* base, uint32_t h, uint32_t& pf0, uint32_t& pf1) {
+  const uint32_t off = node_offset(__builtin_amdgcn_readfirstlane(h));
   const uint64_t b = (uint64_t)base;
   const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
@@ -551,7 +559,7 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
       uint32_t q4;
       {
         const uint32_t top = uniform(lds_stack[sp > 0 ? sp - 1 : 0]);
-        uint32_t off = 64u * (is_leaf(top) ? (uint32_t)P.n_nodes + leaf_first(top) : top);
+        uint32_t off = is_leaf(top) ? 64u * ((uint32_t)P.n_nodes + leaf_first(top)) : node_offset(top);
         off = sp > 0 ? off : 0u;
         asm volatile("s_load_dword %0, %1, %2" : "=&s"(q4) : "s"(P.nodes), "s"(uniform(off)) : "memory");
       }
@@ -781,7 +789,7 @@ __device__ __forceinline__ void traverse_lane(const DevScene& P, const Ray& r, b
   for (;;) {
     // descend interior nodes until this lane holds a leaf or has nothing left
     while (!done && !is_leaf(node)) {
-      const Node64 nd = vload64(P.nodes, node);
+      const Node64 nd = vload64(P.nodes, node_index(node));
       if (STATS) cnt[ST_NODE]++;
       const float tcut = ANY ? INFINITY : h.t;
       const Span s0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
@@ -1902,6 +1910,12 @@ int device_upload(rt_scene* s) {
         nd.pad1 = pf(nd.child1) | ((order >> 6) & 0x3u);
       }
     }
+    if (RT_BYTE_HANDLES) {  // interior children as byte offsets of their records (node_offset)
+      for (Node64& nd : nodes) {
+        if (!is_leaf(nd.child0)) nd.child0 *= 64u;
+        if (!is_leaf(nd.child1)) nd.child1 *= 64u;
+      }
+    }
     if (nn) HIPCHECK(hipMemcpy(s->d_nodes, nodes.data(), nn * 64, hipMemcpyHostToDevice));
     s->d_tris = reinterpret_cast<TriRec64*>(s->d_nodes + nn);
     if (nt) HIPCHECK(hipMemcpy(s->d_tris, hs.tris.data(), nt * 64, hipMemcpyHostToDevice));
@@ -1968,7 +1982,7 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.fshade = s->d_fshade;
   P.sc.refbox = s->d_refbox;
   P.sc.mats = s->d_mats;
-  P.sc.root = hs.root;
+  P.sc.root = (RT_BYTE_HANDLES && !is_leaf(hs.root)) ? hs.root * 64u : hs.root;
   P.sc.n_nodes = (int32_t)hs.nodes.size();
   P.sc.nodes4 = s->d_nodes4;
   P.sc.root4 = 0;
