@@ -1411,10 +1411,10 @@ __device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r
             clamp01(direct0.z + refl.z * st.ks.z)};
 }
 
-// Occupancy of the FULL megakernel, by scene: 8 waves per SIMD (64 VGPR + a 272-B spill) for scenes
+// Occupancy of the FULL megakernel, by scene: 8 waves per SIMD (64 VGPR + a 144-B spill) for scenes
 // whose node + triangle records exceed the chip's aggregate L2 (the 1M soup: 8 waves beat 5 by 18% and
-// 3 by 24% -- the traversal waits on L2 misses and needs the waves), 5 waves (96 VGPR, 76 B spill) for
-// smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident, the spill traffic costs more).
+// 3 by 24% -- the traversal waits on L2 misses and needs the waves), a 5-wave bound (79 VGPR, no
+// spill, so 6 waves) for smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident).
 #ifndef RT_FULL_WAVES_PER_EU
 #define RT_FULL_WAVES_PER_EU 8
 #endif
@@ -1422,11 +1422,15 @@ __device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r
 #define RT_FULL_WAVES_PER_EU_SMALL 5
 #endif
 constexpr size_t kFullSmallSceneBytes = 32u << 20;  // 8 XCDs x 4 MiB L2
+#ifndef RT_FULL_WPB
+#define RT_FULL_WPB 1  // waves per block of the FULL megakernel (1: one 8x8 wave per block, measured
+                       // +6.5% on bunny FULL and +8% on the soup over 4 = one 16x16 tile per block)
+#endif
 template <bool STATS, bool HITS, int TRAV, int WPE = RT_FULL_WAVES_PER_EU>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+__global__ __launch_bounds__(64 * RT_FULL_WPB) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_render_full(FrameParams P) {
   __shared__ WaveLds<TRAV, STATS> lds;
-  const PixelCoord c = pixel_coord(P);
+  const PixelCoord c = pixel_coord<RT_FULL_WPB>(P);
   const bool active = c.active;
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
   const Ray r = primary_ray(P, c.px, c.py);
@@ -1434,8 +1438,8 @@ void k_render_full(FrameParams P) {
 
   Hit h;
   uint32_t face0;
-  const f3 col = RT_FULL_LOOP ? trace_full_loop<STATS, TRAV>(P, r, active, lds, c.wv, cnt, h, face0)
-                              : trace_full<STATS, TRAV>(P, r, active, lds, c.wv, cnt, h, face0);
+  const f3 col = RT_FULL_LOOP ? trace_full_loop<STATS, TRAV>(P, r, active, lds, c.slot, cnt, h, face0)
+                              : trace_full<STATS, TRAV>(P, r, active, lds, c.slot, cnt, h, face0);
   const bool hit0 = face0 != 0xFFFFFFFFu;
   if (active) {
     const size_t pix = (size_t)c.py * P.W + c.px;
@@ -2073,11 +2077,12 @@ static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int tra
 }
 template <bool STATS, bool HITS>
 static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav, bool small) {
-  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_VGPR>), dim3(grid), dim3(256), 0, st, P);
+  const dim3 g(grid * (4 / RT_FULL_WPB)), b(64 * RT_FULL_WPB);
+  if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_VGPR>), g, b, 0, st, P);
   else if (trav == TRAV_B2_LDS && !STATS && small)
-    hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS, RT_FULL_WAVES_PER_EU_SMALL>), dim3(grid), dim3(256), 0, st, P);
-  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS>), dim3(grid), dim3(256), 0, st, P);
-  else hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_W4>), dim3(grid), dim3(256), 0, st, P);
+    hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS, RT_FULL_WAVES_PER_EU_SMALL>), g, b, 0, st, P);
+  else if (trav == TRAV_B2_LDS) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS>), g, b, 0, st, P);
+  else hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_W4>), g, b, 0, st, P);
 }
 
 template <bool STATS>
