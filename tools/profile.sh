@@ -18,7 +18,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ
            ${EXTRA_PMC:-}; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set -d $OUT/pmc$i -o run --output-format csv -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu --no-stats > $OUT/pmc$i.json 2> $OUT/pmc$i.err
+      python3 bench.py ${PMC_ARGS:---steps 5 --warmup 1 --no-cpu --no-stats} > $OUT/pmc$i.json 2> $OUT/pmc$i.err
   rc=$?; echo "pmc$i ($set) rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac
 done
