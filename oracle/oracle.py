@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_LIB_PATH = os.environ.get("RT_ORACLE_LIB") or os.path.join(_HERE, "build", "liboracle.so")
 _lib = None
 
 F32P = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
@@ -169,11 +169,14 @@ class Scene:
         lib().orc_shadow(self.h, len(P), P, L, out)
         return out
 
-    def render(self, cam, lights, W, H, full=False, pixels=None, threads=1, dir_lights=()):
+    def render(self, cam, lights, W, H, full=False, pixels=None, threads=1, dir_lights=(), max_depth=None):
         """lights: [(pos3, color3), ...] point lights; dir_lights: [(vector3, color3), ...] directional lights
-        (Flyscene::dirLights). Returns rgb [n,3], face [n], t [n] (n = W*H or len(pixels))."""
+        (Flyscene::dirLights). max_depth overrides traceRay's recursion limit (flyscene.hpp:142; FULL = 2
+        with shadows, PRIMARY = 1 without). Returns rgb [n,3], face [n], t [n] (n = W*H or len(pixels))."""
         opts = RenderOpts()
         lib().orc_render_opts_default(C.byref(opts), 1 if full else 0)
+        if max_depth is not None:
+            opts.max_depth = max_depth
         D6 = np.ascontiguousarray(np.array([list(p) + list(c) for p, c in dir_lights], np.float32).reshape(-1))
         opts.dir_lights6 = D6.ctypes.data if len(dir_lights) else None
         opts.n_dir_lights = len(dir_lights)

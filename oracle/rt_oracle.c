@@ -549,10 +549,24 @@ typedef struct {
   int32_t* faces; int32_t n, cap;
 } obox;
 
+/* Per-face record in reference iteration order (box creation order, then in-box order): the inputs
+ * calculateDistance reads for one face, stored contiguously so a ray streams through them. Data
+ * placement only: every value is the same float the indexed arrays hold (fnn, fdist, wv). */
+typedef struct {
+  float fn[3], fd;
+  float w0[3], w1[3], w2[3];
+  int32_t f;
+} ofrec;
+
 struct orc_scene {
   orc_mesh* m;
   obox* boxes; int32_t nb, cap;
   int32_t* pass_counts; int32_t npass;
+  /* trace layout (built once after the partition): box bounds as structure-of-arrays for the
+   * vectorised intersectBox sweep, face records in iteration order, boff[b] = first record of box b */
+  float* bsoa;   /* [6][nb]: low x, low y, low z, high x, high y, high z */
+  int32_t* boff; /* [nb + 1] */
+  ofrec* fr;     /* [nf] */
 };
 
 static void box_reshape(obox* b) { for (int k = 0; k < 3; k++) b->shape[k] = b->high[k] - b->low[k]; } /* BoundingBox.cpp:18-24 */
@@ -652,6 +666,35 @@ static int box_split(orc_scene* s, int32_t bi) {
   return 1;
 }
 
+static void scene_trace_layout(orc_scene* s) {
+  const orc_mesh* m = s->m;
+  const int32_t nb = s->nb;
+  s->bsoa = (float*)malloc(sizeof(float) * 6 * (size_t)(nb ? nb : 1));
+  s->boff = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nb + 1));
+  s->fr = (ofrec*)malloc(sizeof(ofrec) * (size_t)(m->nf ? m->nf : 1));
+  int32_t off = 0;
+  for (int32_t b = 0; b < nb; b++) {
+    const obox* bx = &s->boxes[b];
+    for (int k = 0; k < 3; k++) {
+      s->bsoa[(size_t)k * nb + b] = bx->low[k];
+      s->bsoa[(size_t)(3 + k) * nb + b] = bx->high[k];
+    }
+    s->boff[b] = off;
+    for (int32_t i = 0; i < bx->n; i++) {
+      const int32_t f = bx->faces[i];
+      const uint32_t* id = &m->f[3 * (size_t)f];
+      ofrec* r = &s->fr[off++];
+      memcpy(r->fn, &m->fnn[3 * (size_t)f], 12);
+      r->fd = m->fdist[f];
+      memcpy(r->w0, &m->wv[3 * (size_t)id[0]], 12);
+      memcpy(r->w1, &m->wv[3 * (size_t)id[1]], 12);
+      memcpy(r->w2, &m->wv[3 * (size_t)id[2]], 12);
+      r->f = f;
+    }
+  }
+  s->boff[nb] = off;
+}
+
 int orc_scene_build(orc_mesh* m, int32_t min_faces, int32_t max_boxes, orc_scene** out) {
   orc_scene* s = (orc_scene*)calloc(1, sizeof *s);
   s->m = m;
@@ -678,6 +721,7 @@ int orc_scene_build(orc_mesh* m, int32_t min_faces, int32_t max_boxes, orc_scene
       }
     }
   }
+  scene_trace_layout(s);
   *out = s;
   return 0;
 }
@@ -685,7 +729,9 @@ int orc_scene_build(orc_mesh* m, int32_t min_faces, int32_t max_boxes, orc_scene
 void orc_scene_free(orc_scene* s) {
   if (!s) return;
   for (int32_t i = 0; i < s->nb; i++) free(s->boxes[i].faces);
-  free(s->boxes); free(s->pass_counts); free(s);
+  free(s->boxes); free(s->pass_counts);
+  free(s->bsoa); free(s->boff); free(s->fr);
+  free(s);
 }
 int32_t orc_scene_box_count(const orc_scene* s) { return s->nb; }
 void orc_scene_boxes(const orc_scene* s, float* bounds6, int32_t* counts, int32_t* face_order) {
@@ -785,11 +831,30 @@ static int intersect_box(const oray* r, const obox* b) {
   return !(tin > tout || tout < 0);
 }
 
-/* interpolateNormal (flyscene.cpp:572-600) */
-static void interpolate_normal(const orc_mesh* m, int32_t f, const float* P, float* out) {
+/* intersectBox for boxes [b0, b0+n) of the flat list: acc[i] = intersectBox(box b0+i). The same
+ * expressions as intersect_box per box, over the structure-of-arrays bounds so that the compiler
+ * vectorises the sweep (IEEE division and compares are exact in SIMD lanes; s_min/s_max map to
+ * minps/maxps with the operand order that keeps std::min/max's NaN behaviour). */
+__attribute__((target_clones("avx2", "default")))
+static void intersect_boxes(const orc_scene* s, const oray* r, int32_t b0, int32_t n, uint8_t* acc) {
+  const int32_t nb = s->nb;
+  const float *lx = s->bsoa + b0, *ly = s->bsoa + (size_t)nb + b0, *lz = s->bsoa + 2 * (size_t)nb + b0;
+  const float *hx = s->bsoa + 3 * (size_t)nb + b0, *hy = s->bsoa + 4 * (size_t)nb + b0, *hz = s->bsoa + 5 * (size_t)nb + b0;
+  const float ox = r->o2[0], oy = r->o2[1], oz = r->o2[2], dx = r->d2[0], dy = r->d2[1], dz = r->d2[2];
+  for (int32_t i = 0; i < n; i++) {
+    const float ax = (lx[i] - ox) / dx, bx = (hx[i] - ox) / dx;
+    const float ay = (ly[i] - oy) / dy, by = (hy[i] - oy) / dy;
+    const float az = (lz[i] - oz) / dz, bz = (hz[i] - oz) / dz;
+    const float tin = s_max(s_min(ax, bx), s_max(s_min(ay, by), s_min(az, bz)));
+    const float tout = s_min(s_max(ax, bx), s_min(s_max(ay, by), s_max(az, bz)));
+    acc[i] = (uint8_t)!(tin > tout || tout < 0);
+  }
+}
+
+/* interpolateNormal (flyscene.cpp:572-600) for face f with world vertices v0..v2 and unit face normal fn */
+static void interpolate_normal_v(const orc_mesh* m, int32_t f, const float* v0, const float* v1, const float* v2,
+                                 const float* fn, const float* P, float* out) {
   const uint32_t* id = &m->f[3 * f];
-  const float *v0 = &m->wv[3 * id[0]], *v1 = &m->wv[3 * id[1]], *v2 = &m->wv[3 * id[2]];
-  const float* fn = &m->fnn[3 * f];
   float e0[3], e1[3], e2[3], i0[3], i1[3], i2[3], a0[3], a1[3], a2[3];
   e_sub(v1, v0, e0); e_sub(v2, v1, e1); e_sub(v0, v2, e2);
   e_sub(P, v0, i0); e_sub(P, v1, i1); e_sub(P, v2, i2);
@@ -803,6 +868,10 @@ static void interpolate_normal(const orc_mesh* m, int32_t f, const float* P, flo
   float s[3];
   for (int k = 0; k < 3; k++) s[k] = (n0[k] * area1 / area + n1[k] * area2 / area) + n2[k] * area0 / area;
   e_normalized(s, out);
+}
+static void interpolate_normal(const orc_mesh* m, int32_t f, const float* P, float* out) {
+  const uint32_t* id = &m->f[3 * f];
+  interpolate_normal_v(m, f, &m->wv[3 * id[0]], &m->wv[3 * id[1]], &m->wv[3 * id[2]], &m->fnn[3 * f], P, out);
 }
 
 /* calculateDistance (flyscene.cpp:444-478): returns t (or -1), P */
@@ -819,20 +888,47 @@ static float calc_distance(const orc_mesh* m, const float* o, const float* d, in
   return t;
 }
 
-/* calculateMinimumFace (flyscene.cpp:373-396) */
+/* calculateDistance on an iteration-order face record (same arithmetic as calc_distance) */
+static inline float calc_distance_rec(const orc_mesh* m, const ofrec* fr, const float* o, const float* d, float* P) {
+  if (e_dot(fr->fn, d) == 0) return -1.0f;
+  float orth = fr->fd - e_dot(o, fr->fn);
+  float t = orth / e_dot(d, fr->fn);
+  float p[3] = {o[0] + t * d[0], o[1] + t * d[1], o[2] + t * d[2]};
+  /* interpolateNormal's inside test first (its early return, flyscene.cpp:584-586); the rest of it
+   * only for points that pass */
+  float e0[3], e1[3], e2[3], i0[3], i1[3], i2[3], a0[3], a1[3], a2[3];
+  e_sub(fr->w1, fr->w0, e0); e_sub(fr->w2, fr->w1, e1); e_sub(fr->w0, fr->w2, e2);
+  e_sub(p, fr->w0, i0); e_sub(p, fr->w1, i1); e_sub(p, fr->w2, i2);
+  e_cross(e0, i0, a0); e_cross(e1, i1, a1); e_cross(e2, i2, a2);
+  if (e_dot(fr->fn, a0) < 0 || e_dot(fr->fn, a1) < 0 || e_dot(fr->fn, a2) < 0) return -1.0f;
+  float n[3];
+  interpolate_normal_v(m, fr->f, fr->w0, fr->w1, fr->w2, fr->fn, p, n);
+  if (e_norm(n) == 0) return -1.0f;
+  if (P) memcpy(P, p, 12);
+  return t;
+}
+
+#define ORC_BOX_CHUNK 512
+
+/* calculateMinimumFace (flyscene.cpp:373-396): boxes in creation order, faces in in-box order, the
+ * first minimum kept (strict <) */
 static int32_t closest(const orc_scene* s, const float* o, const float* d, float* tbest, float* Pbest) {
   const orc_mesh* m = s->m;
   oray r; obj_ray(m, o, d, &r);
   float best = INFINITY;
   int32_t bf = -1;
   float P[3] = {0, 0, 0}, Pc[3];
-  for (int32_t bi = 0; bi < s->nb; bi++) {
-    const obox* b = &s->boxes[bi];
-    if (!intersect_box(&r, b)) continue;
-    for (int32_t i = 0; i < b->n; i++) {
-      int32_t f = b->faces[i];
-      float t = calc_distance(m, o, d, f, Pc);
-      if (0 <= t && t < best) { best = t; bf = f; memcpy(P, Pc, 12); }
+  uint8_t acc[ORC_BOX_CHUNK];
+  for (int32_t b0 = 0; b0 < s->nb; b0 += ORC_BOX_CHUNK) {
+    const int32_t n = s->nb - b0 < ORC_BOX_CHUNK ? s->nb - b0 : ORC_BOX_CHUNK;
+    intersect_boxes(s, &r, b0, n, acc);
+    for (int32_t i = 0; i < n; i++) {
+      if (!acc[i]) continue;
+      const int32_t bi = b0 + i;
+      for (int32_t k = s->boff[bi]; k < s->boff[bi + 1]; k++) {
+        float t = calc_distance_rec(m, &s->fr[k], o, d, Pc);
+        if (0 <= t && t < best) { best = t; bf = s->fr[k].f; memcpy(P, Pc, 12); }
+      }
     }
   }
   *tbest = best;
@@ -846,11 +942,16 @@ static int shadow(const orc_scene* s, const float* P, const float* L) {
   float inter[3];
   for (int k = 0; k < 3; k++) inter[k] = P[k] + 0.003f * L[k];
   oray r; obj_ray(m, P, L, &r);
-  for (int32_t bi = 0; bi < s->nb; bi++) {
-    const obox* b = &s->boxes[bi];
-    if (!intersect_box(&r, b)) continue;
-    for (int32_t i = 0; i < b->n; i++)
-      if (calc_distance(m, inter, L, b->faces[i], NULL) >= 0) return 1;
+  uint8_t acc[ORC_BOX_CHUNK];
+  for (int32_t b0 = 0; b0 < s->nb; b0 += ORC_BOX_CHUNK) {
+    const int32_t n = s->nb - b0 < ORC_BOX_CHUNK ? s->nb - b0 : ORC_BOX_CHUNK;
+    intersect_boxes(s, &r, b0, n, acc);
+    for (int32_t i = 0; i < n; i++) {
+      if (!acc[i]) continue;
+      const int32_t bi = b0 + i;
+      for (int32_t k = s->boff[bi]; k < s->boff[bi + 1]; k++)
+        if (calc_distance_rec(m, &s->fr[k], inter, L, NULL) >= 0) return 1;
+    }
   }
   return 0;
 }
