@@ -13,6 +13,13 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unu
 OBJ      := $(PKG)/build
 LIB      := $(PKG)/lib/librtamd.so
 HDRS     := include/rt/rt_api.h $(wildcard $(PKG)/csrc/*.h)
+# source hash embedded in the library (rt_source_hash(); rtamd.source_hash() recomputes it from the tree)
+SRCS     := $(sort $(wildcard $(PKG)/csrc/*.hip $(PKG)/csrc/*.cpp $(PKG)/csrc/*.h) include/rt/rt_api.h)
+SRC_HASH := $(shell cat $(SRCS) | sha256sum | cut -c1-16)
+VERSION_H := $(OBJ)/rt_version.h
+# rewritten only when the hash changes, so unchanged sources do not relink
+$(shell mkdir -p $(OBJ) && echo '#define RT_SOURCE_HASH "$(SRC_HASH)"' > $(VERSION_H).new && \
+        (cmp -s $(VERSION_H).new $(VERSION_H) || cp $(VERSION_H).new $(VERSION_H)); rm -f $(VERSION_H).new)
 
 all: $(LIB) oracle cli
 
@@ -32,20 +39,23 @@ $(OBJ)/rt_boxes.o: $(PKG)/csrc/rt_boxes.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(OBJ)/rt_version.o: $(PKG)/csrc/rt_version.cpp $(VERSION_H) include/rt/rt_api.h
+	$(CXX) $(CXXFLAGS) -I$(OBJ) -c $< -o $@
+
 $(OBJ)/rt_cache.o: $(PKG)/csrc/rt_cache.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o
+$(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o
 	@mkdir -p $(PKG)/lib
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
 # A/B builds of the same sources with extra device flags (experiments only):
 #   make ablib TAG=noslp EXTRA="-fno-slp-vectorize"  ->  lib/librtamd_noslp.so  (select with RTAMD_LIB)
-ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o
+ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o
 	@mkdir -p $(OBJ) $(PKG)/lib
 	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $(OBJ)/rt_device_$(TAG).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o -lpthread
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o -lpthread
 
 cli: $(PKG)/lib/rt_render_cli
 

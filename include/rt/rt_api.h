@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 1
+#define RT_API_VERSION 2
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -212,7 +212,14 @@ typedef struct rt_frame {
                           t % shard_count == shard_index */
   int32_t shard_count; /* 1 = whole frame */
   int32_t flags;       /* RT_FRAME_* */
+  int32_t max_depth;   /* traceRay's recursion limit (Flyscene::max_depth, flyscene.hpp:142; the reference
+                          fixes 2): 0 = the mode's own (PRIMARY 1, FULL 2); 1..RT_MAX_TRACE_DEPTH = trace
+                          that many levels (primary hit + max_depth-1 reflection bounces), with shadow rays
+                          in FULL mode and without in PRIMARY mode. The FULL/2 and PRIMARY/1 cases run the
+                          tuned kernels; other depths one generic kernel (same arithmetic, same bits). */
 } rt_frame;
+
+#define RT_MAX_TRACE_DEPTH 16
 
 #define RT_FRAME_WRITE_HITS 1 /* also record per-pixel face index and t (rt_frame_download) */
 #define RT_FRAME_STATS 2      /* counting run: per-ray node visits / triangle tests (slower) */
@@ -243,13 +250,15 @@ int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, i
                     const rt_frame* frame);
 int rt_synchronize(rt_scene* s, rt_stats* stats);
 /* copies the last frame from the device: rgb [H][W][3]; face [H][W] (-1 miss) and t [H][W] need
- * RT_FRAME_WRITE_HITS. NULL = skip. */
-int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t);
+ * RT_FRAME_WRITE_HITS. NULL = skip. capacity_pixels: the pixels each given buffer holds; smaller than
+ * the last frame's W x H -> RT_ERR_INVALID, nothing written. */
+int rt_frame_download(rt_scene* s, int64_t capacity_pixels, float* rgb, int32_t* face, float* t);
 /* Output path: the last frame converted on the device to writePPMImage's 8-bit
  * values min(255, (int)(255*c)) and downloaded at 3 B/px. *exact (may be NULL) = 1 when every value
  * was in 0..255, i.e. the bytes are exactly the PPM's numbers; 0 when some colour was NaN or negative
- * (clamped to 0 here; rt_frame_download + rt_write_ppm reproduce the reference's text then). */
-int rt_frame_download_rgb8(rt_scene* s, uint8_t* rgb8, int32_t* exact);
+ * (clamped to 0 here; rt_frame_download + rt_write_ppm reproduce the reference's text then).
+ * capacity_pixels: pixels the buffer holds (3 bytes each), checked as in rt_frame_download. */
+int rt_frame_download_rgb8(rt_scene* s, int64_t capacity_pixels, uint8_t* rgb8, int32_t* exact);
 
 /* Multi-GPU frame assembly (f3). Each rank's slice holds the 8-bit values of its own 16x16 tiles
  * (rt_frame.shard_index/shard_count of its last frame) in shard tile order, rt_frame_shard_bytes() long
@@ -292,6 +301,12 @@ int rt_debug_ray(rt_scene* s, const rt_camera* cam, const rt_light* lights, int3
  * ------------------------------------------------------------------------------------------- */
 int rt_device_count(void);       /* 0 when no GPU is visible */
 int rt_version(void);            /* RT_API_VERSION */
+/* "librtamd api <N> gfx950 sources <hash>": the build's identity. rt_source_hash() is the hash alone:
+ * SHA-256 (first 16 hex digits) of the product sources this library was built from (csrc/*.hip,
+ * *.cpp, *.h and include/rt/rt_api.h, concatenated in sorted path order), so a record can show that
+ * the binary it ran matches the tree it came from. */
+const char* rt_version_string(void);
+const char* rt_source_hash(void);
 const char* rt_last_error(void); /* thread-local */
 
 /* Verification hooks (tests only; never used by the render path): evaluate the Eigen-order float

@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <utility>
+#include <vector>
 
 #include "rt_scene.h"
 
@@ -233,6 +235,58 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
     for (int c = 0; c < 4; c++)
       if (((n.valid >> c) & 1) && !handle_ok(n.child[c], h.n_nodes4)) { rt::set_error("rt_scene_load: bad wide BVH"); return RT_ERR_IO; }
   if (h.nf > 0 && !handle_ok(h.root, h.n_nodes)) { rt::set_error("rt_scene_load: bad BVH root"); return RT_ERR_IO; }
+  // Shape checks (the content hash is not a signature: a crafted file can carry a valid one). Each
+  // tree must be a tree: walked from its root, every interior node is reached exactly once (no
+  // cycle, no shared subtree), and its depth is recomputed here, never taken from the header, then
+  // held to rt_scene_create's limits: the binary tree within the 64-entry wave stack, the wide tree
+  // within kStack4 (else it is dropped and the binary traversal runs), and at most kMaxFaces faces
+  // (32-bit byte offsets of the records).
+  if ((uint32_t)h.nf > rt::kMaxFaces) { rt::set_error("rt_scene_load: %d faces exceed the %u-face limit", h.nf, rt::kMaxFaces); return RT_ERR_IO; }
+  {
+    std::vector<uint8_t> seen(hs.nodes.size(), 0);
+    std::vector<std::pair<uint32_t, int>> st;
+    int depth = 0;
+    if (!hs.nodes.empty() && !rt::is_leaf(h.root)) st.push_back({h.root, 1});
+    while (!st.empty()) {
+      const auto [n, d] = st.back();
+      st.pop_back();
+      if (seen[n]++) { rt::set_error("rt_scene_load: BVH node %u reached twice (not a tree)", n); return RT_ERR_IO; }
+      depth = std::max(depth, d + 1);
+      if (depth > rt::kMaxDepth + 2) { rt::set_error("rt_scene_load: BVH deeper than the traversal stack"); return RT_ERR_IO; }
+      const rt::Node64& nd = hs.nodes[n];
+      if (!rt::is_leaf(nd.child1)) st.push_back({nd.child1, d + 1});
+      if (!rt::is_leaf(nd.child0)) st.push_back({nd.child0, d + 1});
+    }
+    if (hs.nodes.empty() || rt::is_leaf(h.root)) {  // no interior node: nothing for the stack to hold
+      if (h.depth < 0 || h.depth > 2) { rt::set_error("rt_scene_load: bad BVH depth"); return RT_ERR_IO; }
+      hs.depth = h.depth;
+    } else {
+      hs.depth = depth;
+    }
+  }
+  {
+    std::vector<uint8_t> seen(hs.nodes4.size(), 0);
+    std::vector<std::pair<uint32_t, int>> st;
+    int maxd = -1;
+    bool ok4 = true;
+    if (!hs.nodes4.empty()) st.push_back({0u, 0});
+    while (!st.empty() && ok4) {
+      const auto [n, d] = st.back();
+      st.pop_back();
+      if (seen[n]++) { ok4 = false; break; }
+      maxd = std::max(maxd, d);
+      if (3 * (maxd + 1) + 4 > rt::kStack4) { ok4 = false; break; }
+      const rt::Node4Q& nd = hs.nodes4[n];
+      for (int c = 0; c < 4; c++)
+        if (((nd.valid >> c) & 1) && !rt::is_leaf(nd.child[c])) st.push_back({nd.child[c], d + 1});
+    }
+    if (!ok4) {  // not a tree or too deep for the wide stack: keep the binary traversal only
+      hs.nodes4.clear();
+      hs.depth4 = 0;
+    } else {
+      hs.depth4 = hs.nodes4.empty() ? 0 : maxd + 1;
+    }
+  }
   s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (s->opts.device != RT_DEVICE_NONE) {
     const int rc = rt::device_upload(s.get());

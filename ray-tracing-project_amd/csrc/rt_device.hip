@@ -1454,6 +1454,96 @@ void k_render_full(FrameParams P) {
   if (STATS) flush_stats(P, cnt, c.lane);
 }
 
+// traceRay(o, d, 0) for any recursion limit D = P.max_depth (flyscene.cpp:317-371; the reference fixes
+// max_depth = 2 at flyscene.hpp:142, SURVEY 8(b) b2 exposes it): level d traces the closest hit of
+// the ray from level d-1's reflection, shades it (calculateColor, shadows per P.shadows) and updates
+// the sticky ks (traceRay :355-358). The reference combines on the way back up,
+//   colour_d = clamp01(direct_d + colour_{d+1} (*) ks),
+// reading the ks member AFTER the deeper levels returned, i.e. the last value any level wrote; so the
+// kernel keeps each level's direct colour (lane-private array, D <= RT_MAX_TRACE_DEPTH) and folds them
+// from the deepest hit level upwards with that final ks. The deepest hit level adds 0 (*) ks (its own
+// reflection returned black: a miss below depth 0, or depth == max_depth). D = 0 returns black for
+// every pixel without tracing (traceRay :318-320). Same expressions and order as k_render_full for
+// D = 2, hence the same bits (tested); this kernel serves the other depths.
+template <bool STATS, bool HITS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU_SMALL)))
+void k_render_depth(FrameParams P) {
+  __shared__ WaveLds<TRAV_B2_LDS, STATS> lds;
+  const PixelCoord c = pixel_coord<1>(P);
+  const bool active = c.active;
+  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  Ray cur = primary_ray(P, c.px, c.py);
+  const Ray r0 = cur;
+  if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
+  MatState st = load_mat(P.defmat);
+  f3 direct[RT_MAX_TRACE_DEPTH];
+  int levels = 0;  // levels whose closest hit exists (the chain stops at the first miss)
+  bool act = active;
+  Hit h0{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  uint32_t face0 = 0xFFFFFFFFu;
+  const int D = P.max_depth;
+#pragma clang loop unroll(disable)
+  for (int d = 0; d < D; d++) {
+    Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    bool dummy = false;
+    if (d == 0) trace_oct<false, STATS, TRAV_B2_LDS>(P.sc, cur, act, h, dummy, lds, c.slot, cnt);
+    else trace<false, STATS, TRAV_B2_LDS>(P.sc, cur, act, h, dummy, lds, c.slot, cnt);
+    const bool hit = act && h.t != INFINITY;
+    if (STATS && d == 0 && hit) cnt[ST_HITS]++;
+    HitInfo hi;
+    hi.mat = -1;
+    hi.face = 0xFFFFFFFFu;
+    hi.p = f3{0.0f, 0.0f, 0.0f};
+    hi.n = f3{0.0f, 0.0f, 0.0f};
+    if (hit) {
+      const TriRec64 tr = vload_tri(P.sc.tris, h.slot);
+      hi.face = tr.face;
+      hi.p = f3{cur.o.x + h.t * cur.d.x, cur.o.y + h.t * cur.d.y, cur.o.z + h.t * cur.d.z};
+      hi.n = hit_normal(P.sc, tr, hi.p, hi.mat);
+    }
+    if (d == 0) {
+      h0 = h;
+      face0 = hit ? hi.face : 0xFFFFFFFFu;
+    }
+    const f3 dc = P.shadows ? calc_color<true, STATS, TRAV_B2_LDS>(P, st, hi, cur.o, hit, &lds, c.slot, cnt)
+                            : calc_color<false, STATS, TRAV_B2_LDS>(P, st, hi, cur.o, hit, &lds, c.slot, cnt);
+    if (hit) {
+      direct[d] = dc;
+      levels = d + 1;
+      if (hi.mat != -1) st.ks = load_mat(P.sc.mats[hi.mat]).ks;  // traceRay :355-358
+    }
+    if (d + 1 == D) break;  // traceRay(depth + 1) returns black without tracing (:318-320)
+    // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
+    Ray rr;
+    rr.d = reflect(normalized(cur.d), hi.n);
+    rr.o = offset(hi.p, rr.d, 0.001f);
+    rr.o2 = affv3(P.Minv, rr.o);
+    rr.d2 = normalized(m3v3(P.MS, rr.d));
+    setup_cull(rr);
+    if (STATS && hit) cnt[ST_TOTAL]++;
+    cur = rr;
+    act = hit;
+    if (ballot(act) == 0) break;  // no lane of the wave continues
+  }
+  f3 col{0.0f, 0.0f, 0.0f};
+  for (int d = levels - 1; d >= 0; d--)
+    col = f3{clamp01(direct[d].x + col.x * st.ks.x), clamp01(direct[d].y + col.y * st.ks.y),
+             clamp01(direct[d].z + col.z * st.ks.z)};
+  if (D > 0 && levels == 0) col = f3{P.bg[0], P.bg[1], P.bg[2]};  // primary miss: BACKGROUND_COLOR (:327-332)
+  (void)r0;
+  if (active) {
+    const size_t pix = (size_t)c.py * P.W + c.px;
+    P.rgb[3 * pix + 0] = col.x;
+    P.rgb[3 * pix + 1] = col.y;
+    P.rgb[3 * pix + 2] = col.z;
+    if (HITS) {
+      P.face_out[pix] = face0 != 0xFFFFFFFFu ? (int32_t)face0 : -1;
+      P.t_out[pix] = h0.t;
+    }
+  }
+  if (STATS) flush_stats(P, cnt, c.lane);
+}
+
 // ------------------------------------------------------------------------------------------------
 // FULL as a wavefront pipeline: k_render_full's work cut at every traversal into lean stage kernels
 // (each at full occupancy) that hand per-pixel records through HBM:
@@ -2170,6 +2260,10 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     return RT_ERR_INVALID;
   }
   if (fr->mode != RT_MODE_PRIMARY && fr->mode != RT_MODE_FULL) { set_error("rt_render: bad mode %d", fr->mode); return RT_ERR_INVALID; }
+  if (fr->max_depth < 0 || fr->max_depth > RT_MAX_TRACE_DEPTH) {
+    set_error("rt_render: max_depth %d outside 0..%d", fr->max_depth, RT_MAX_TRACE_DEPTH);
+    return RT_ERR_INVALID;
+  }
   const int sc = fr->shard_count > 0 ? fr->shard_count : 1;
   const int si = fr->shard_index;
   if (si < 0 || si >= sc) { set_error("rt_render: shard %d of %d", si, sc); return RT_ERR_INVALID; }
@@ -2263,7 +2357,18 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
              ev_b = (hipEvent_t)s->ev_pool[s->ev_used + 2];
   s->ev_used += 3;
   HIPCHECK(hipEventRecord(ev_a, st));
-  if (grid > 0) {
+  const int mode_depth = fr->mode == RT_MODE_FULL ? 2 : 1;
+  const int depth = fr->max_depth > 0 ? fr->max_depth : mode_depth;
+  P.max_depth = depth;
+  P.shadows = fr->mode == RT_MODE_FULL ? 1 : 0;
+  if (grid > 0 && depth != mode_depth) {
+    // any other recursion limit: the generic traceRay kernel (one 8x8 wave per block)
+    const dim3 g(grid * 4), b(64);
+    if (stats) { if (hits) hipLaunchKernelGGL((k_render_depth<true, true>), g, b, 0, st, P); else hipLaunchKernelGGL((k_render_depth<true, false>), g, b, 0, st, P); }
+    else { if (hits) hipLaunchKernelGGL((k_render_depth<false, true>), g, b, 0, st, P); else hipLaunchKernelGGL((k_render_depth<false, false>), g, b, 0, st, P); }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventRecord(ev_m, st));
+  } else if (grid > 0) {
     if (fr->mode == RT_MODE_PRIMARY && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
       const dim3 g(grid * (4 / RT_TRACE_WPB)), b(64 * RT_TRACE_WPB);
       if (hits) hipLaunchKernelGGL(k_primary_fused<true>, g, b, 0, st, P);
@@ -2365,13 +2470,18 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
   return RT_OK;
 }
 
-extern "C" int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* t) {
+extern "C" int rt_frame_download(rt_scene* s, int64_t capacity_pixels, float* rgb, int32_t* face, float* t) {
   int rc = check_device_scene(s);
   if (rc) return rc;
   const rt_scene::FrameSlot& f = s->slots[s->last_slot];
   HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));
   const size_t npix = (size_t)s->last_W * s->last_H;
   if (!f.d_rgb || npix > f.fb_pixels) { set_error("rt_frame_download: no frame rendered"); return RT_ERR_INVALID; }
+  if (capacity_pixels < (int64_t)npix) {
+    set_error("rt_frame_download: buffers hold %lld pixels, the last frame has %zu (%d x %d)", (long long)capacity_pixels,
+              npix, s->last_W, s->last_H);
+    return RT_ERR_INVALID;
+  }
   if (rgb) HIPCHECK(hipMemcpy(rgb, f.d_rgb, npix * 12, hipMemcpyDeviceToHost));
   if ((face || t) && !(s->last_flags & RT_FRAME_WRITE_HITS)) { set_error("last frame was rendered without RT_FRAME_WRITE_HITS"); return RT_ERR_INVALID; }
   if (face) HIPCHECK(hipMemcpy(face, f.d_face, npix * 4, hipMemcpyDeviceToHost));
@@ -2379,13 +2489,18 @@ extern "C" int rt_frame_download(rt_scene* s, float* rgb, int32_t* face, float* 
   return RT_OK;
 }
 
-extern "C" int rt_frame_download_rgb8(rt_scene* s, uint8_t* rgb8, int32_t* exact) {
+extern "C" int rt_frame_download_rgb8(rt_scene* s, int64_t capacity_pixels, uint8_t* rgb8, int32_t* exact) {
   int rc = check_device_scene(s);
   if (rc) return rc;
   if (!rgb8) { set_error("rt_frame_download_rgb8: null output"); return RT_ERR_INVALID; }
   rt_scene::FrameSlot& f = s->slots[s->last_slot];
   const size_t npix = (size_t)s->last_W * s->last_H;
   if (!f.d_rgb || npix == 0 || npix > f.fb_pixels) { set_error("rt_frame_download_rgb8: no frame rendered"); return RT_ERR_INVALID; }
+  if (capacity_pixels < (int64_t)npix) {
+    set_error("rt_frame_download_rgb8: buffer holds %lld pixels, the last frame has %zu (%d x %d)",
+              (long long)capacity_pixels, npix, s->last_W, s->last_H);
+    return RT_ERR_INVALID;
+  }
   hipStream_t st = (hipStream_t)f.stream;
   if (npix > f.rgb8_pixels) {
     HIPCHECK(hipStreamSynchronize(st));
@@ -2459,9 +2574,9 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* ligh
   if (!out_rgb) return RT_OK;
   const int W = fr->width, H = fr->height;
   const int sc = fr->shard_count > 0 ? fr->shard_count : 1;
-  if (sc == 1) return rt_frame_download(s, out_rgb, nullptr, nullptr);
+  if (sc == 1) return rt_frame_download(s, (int64_t)W * H, out_rgb, nullptr, nullptr);
   std::vector<float> full((size_t)W * H * 3);
-  if ((rc = rt_frame_download(s, full.data(), nullptr, nullptr))) return rc;
+  if ((rc = rt_frame_download(s, (int64_t)W * H, full.data(), nullptr, nullptr))) return rc;
   const int tiles_x = (W + 15) / 16, ntiles = tiles_x * ((H + 15) / 16);
   for (int t = fr->shard_index; t < ntiles; t += sc) {
     const int tx = t % tiles_x, ty = t / tiles_x;

@@ -136,6 +136,8 @@ struct FrameParams {
   int32_t xcd_remap;
   int32_t shard_index, shard_count, n_tiles_shard;
   int32_t mode, flags;
+  int32_t max_depth;          // k_render_depth: traceRay's recursion limit (flyscene.hpp:142)
+  int32_t shadows;            // k_render_depth: shadow() per light (FULL) or not (PRIMARY)
   float* rgb;
   int32_t* face_out;
   float* t_out;

@@ -81,7 +81,7 @@ double Flyscene::raytraceScene(int width, int height) {
     ls[i] = rt_light{{lights[i].first.x, lights[i].first.y, lights[i].first.z},
                      {lights[i].second.x, lights[i].second.y, lights[i].second.z}};
   }
-  rt_frame fr{width, height, mode, 0, 1, 0};
+  rt_frame fr{width, height, mode, 0, 1, 0, 0};
   rt_stats st;
   printf("ray tracing ...\n");
   const auto t0 = std::chrono::steady_clock::now();
@@ -93,12 +93,12 @@ double Flyscene::raytraceScene(int width, int height) {
   }
   std::vector<uint8_t> rgb8((size_t)width * height * 3);
   int32_t exact = 0;
-  int rc = rt_frame_download_rgb8(scene_, rgb8.data(), &exact);
+  int rc = rt_frame_download_rgb8(scene_, (int64_t)width * height, rgb8.data(), &exact);
   if (rc == RT_OK && exact) {
     rc = rt_write_ppm_rgb8(output.c_str(), rgb8.data(), width, height);
   } else if (rc == RT_OK) {
     last_image.assign((size_t)width * height * 3, 0.0f);
-    rc = rt_frame_download(scene_, last_image.data(), nullptr, nullptr);
+    rc = rt_frame_download(scene_, (int64_t)width * height, last_image.data(), nullptr, nullptr);
     if (rc == RT_OK) rc = rt_write_ppm(output.c_str(), last_image.data(), width, height);
   }
   if (rc != RT_OK) fprintf(stderr, "%s\n", rt_last_error());

@@ -28,7 +28,7 @@ EXPORTS = [
     "rt_debug_set_variant", "rt_scene_save", "rt_scene_load",
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
-    "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray",
+    "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
 ]
 
 
@@ -82,7 +82,7 @@ class RandState(C.Structure):
 
 class Frame(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("mode", C.c_int32), ("shard_index", C.c_int32),
-                ("shard_count", C.c_int32), ("flags", C.c_int32)]
+                ("shard_count", C.c_int32), ("flags", C.c_int32), ("max_depth", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -106,6 +106,8 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.rt_last_error.restype = C.c_char_p
+        L.rt_version_string.restype = C.c_char_p
+        L.rt_source_hash.restype = C.c_char_p
         L.rt_mesh_load_obj.argtypes = [C.c_char_p, C.POINTER(vp)]
         L.rt_mesh_from_arrays.argtypes = [C.c_int32, vp, vp, C.c_int32, vp, vp, vp, C.c_int32, vp, C.POINTER(vp)]
         L.rt_mesh_destroy.argtypes = [vp]
@@ -125,7 +127,7 @@ def lib():
         L.rt_render.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.POINTER(Frame), vp, C.POINTER(Stats)]
         L.rt_render_async.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.POINTER(Frame)]
         L.rt_synchronize.argtypes = [vp, C.POINTER(Stats)]
-        L.rt_frame_download.argtypes = [vp, vp, vp, vp]
+        L.rt_frame_download.argtypes = [vp, C.c_int64, vp, vp, vp]
         L.rt_trace_closest.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp]
         L.rt_trace_shadow.argtypes = [vp, C.c_int32, vp, vp, vp]
         L.rt_debug_math_host.argtypes = [C.c_int32, C.c_int32, vp, vp]
@@ -133,7 +135,7 @@ def lib():
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
-        L.rt_frame_download_rgb8.argtypes = [vp, vp, C.POINTER(C.c_int32)]
+        L.rt_frame_download_rgb8.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
         L.rt_frame_shard_bytes.argtypes = [C.c_int32, C.c_int32, C.c_int32]
         L.rt_trace_closest_normal.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, vp]
@@ -167,6 +169,30 @@ class RTError(RuntimeError):
 def check(rc):
     if rc != 0:
         raise RTError(f"librtamd error {rc}: {lib().rt_last_error().decode()}")
+
+
+def source_hash(root=None):
+    """The hash the Makefile embeds (rt_source_hash), recomputed over the product sources in this tree."""
+    import hashlib
+    import glob
+    pkg = HERE if root is None else os.path.join(root, "ray-tracing-project_amd")
+    top = os.path.dirname(pkg)
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(pkg, "csrc", "*.h")) + [os.path.join(top, "include", "rt", "rt_api.h")],
+                   key=lambda p: os.path.relpath(p, top))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_identity():
+    """{"library": rt_version_string(), "source_hash": embedded, "tree_hash": recomputed, "matches_tree": bool}"""
+    emb = lib().rt_source_hash().decode()
+    tree = source_hash()
+    return {"library": lib().rt_version_string().decode(), "source_hash": emb, "tree_hash": tree,
+            "matches_tree": emb == tree}
 
 
 def device_count():
@@ -274,11 +300,20 @@ class Scene:
         check(lib().rt_scene_get_info(self.h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in i._fields_}
 
+    def download(self, W, H, want_hits=False):
+        """The last frame (rt_frame_download): rgb [H,W,3], plus face / t when it was rendered with
+        RT_FRAME_WRITE_HITS and want_hits is set."""
+        rgb = np.zeros((H, W, 3), np.float32)
+        face = np.zeros((H, W), np.int32) if want_hits else None
+        t = np.zeros((H, W), np.float32) if want_hits else None
+        check(lib().rt_frame_download(self.h, W * H, _p(rgb), _p(face), _p(t)))
+        return (rgb, face, t) if want_hits else rgb
+
     def download_rgb8(self, W, H):
         """The last frame as writePPMImage's 8-bit values (device conversion); returns (rgb8, exact)."""
         out = np.zeros((H, W, 3), np.uint8)
         ex = C.c_int32(0)
-        check(lib().rt_frame_download_rgb8(self.h, _p(out), C.byref(ex)))
+        check(lib().rt_frame_download_rgb8(self.h, W * H, _p(out), C.byref(ex)))
         return out, bool(ex.value)
 
     def trace_color(self, o, d, lights):
@@ -360,8 +395,10 @@ class Scene:
             arr[i].kind = l[2] if len(l) > 2 else RT_LIGHT_POINT
         return arr
 
-    def render(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0, want_hits=False):
-        fr = Frame(W, H, mode, shard[0], shard[1], flags | (RT_FRAME_WRITE_HITS if want_hits else 0))
+    def render(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0, want_hits=False, max_depth=0):
+        """rt_render: rgb [H,W,3] (+ face, t with want_hits) and the stats. max_depth: traceRay's recursion
+        limit (0 = the mode's own: PRIMARY 1, FULL 2)."""
+        fr = Frame(W, H, mode, shard[0], shard[1], flags | (RT_FRAME_WRITE_HITS if want_hits else 0), max_depth)
         rgb = np.zeros((H, W, 3), np.float32)
         st = Stats()
         L = self._lights(lights)
@@ -370,13 +407,13 @@ class Scene:
         if want_hits:
             face = np.zeros((H, W), np.int32)
             t = np.zeros((H, W), np.float32)
-            check(lib().rt_frame_download(self.h, None, _p(face), _p(t)))
+            check(lib().rt_frame_download(self.h, W * H, None, _p(face), _p(t)))
             return rgb, face, t, st.as_dict()
         return rgb, st.as_dict()
 
-    def render_async(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0):
+    def render_async(self, cam, lights, W, H, mode=RT_MODE_PRIMARY, shard=(0, 1), flags=0, max_depth=0):
         self._keep = self._lights(lights)
-        fr = Frame(W, H, mode, shard[0], shard[1], flags)
+        fr = Frame(W, H, mode, shard[0], shard[1], flags, max_depth)
         check(lib().rt_render_async(self.h, C.byref(cam), C.cast(self._keep, C.c_void_p), len(lights), C.byref(fr)))
 
     def synchronize(self):

@@ -251,7 +251,7 @@ def test_frames_in_flight_are_independent(rt, soup):
         sc.synchronize()
         c = cams[8 % len(cams)]
         out = np.zeros((c[1], c[0], 3), np.float32)
-        rt.lib().rt_frame_download(sc.h, out.ctypes.data, None, None)
+        rt.lib().rt_frame_download(sc.h, out.shape[0] * out.shape[1], out.ctypes.data, None, None)
         assert out.tobytes() == ref[c].tobytes(), fif
 
 

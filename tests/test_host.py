@@ -20,7 +20,9 @@ def test_header_symbols_exported(rt):
     L = rt.lib()
     for name in sorted(decl):
         assert hasattr(L, name), name
-    assert L.rt_version() == 1
+    assert L.rt_version() == 2
+    ident = rt.build_identity()
+    assert ident["matches_tree"], ident
 
 
 def test_no_device_is_reported_not_faked(rt):
@@ -243,6 +245,83 @@ def test_scene_cache_roundtrip(rt, tmp_path, name):
         bad.write_bytes(damaged)
         with pytest.raises(rt.RTError):
             rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
+
+
+def _cache_sections(raw):
+    """Split a scene cache (rt_cache.cpp) into its written chunks: header, then the arrays in write order."""
+    import struct
+    nv, nf, nm, nb, nbf, nn, nn4, nt = struct.unpack_from("<8i", raw, 16)
+    assert struct.unpack_from("<I", raw, 12)[0] == 256
+    sizes = [256, 12 * nv, 12 * nv, 12 * nf, 4 * nf, 12 * nf, 4 * nf, 48 * nm, 44 * nb, 4 * nbf, 4 * nf, 4 * nf,
+             64 * nn, 64 * nn4, 64 * nt]
+    out, off = [], 0
+    for n in sizes:
+        out.append(bytearray(raw[off:off + n]))
+        off += n
+    assert off + 8 == len(raw)
+    return out
+
+
+def _cache_sign(sections):
+    """Re-assemble a cache with a valid content hash (the Hasher of rt_cache.cpp, chunk by chunk)."""
+    M = (1 << 64) - 1
+    h = 0x9E3779B97F4A7C15
+    for b in sections:
+        n = len(b)
+        if n == 0:
+            continue
+        words = np.frombuffer(bytes(b[: n - n % 8]), "<u8")
+        for w in words.tolist():
+            h = ((h ^ w) * 0xBF58476D1CE4E5B9) & M
+            h ^= h >> 31
+        w = int.from_bytes(bytes(b[n - n % 8:]).ljust(8, b"\0"), "little")
+        h = ((h ^ w ^ n) * 0x94D049BB133111EB) & M
+        h ^= h >> 29
+    return b"".join(bytes(x) for x in sections) + h.to_bytes(8, "little")
+
+
+def test_scene_cache_rejects_crafted_trees(rt, tmp_path):
+    """a cache whose content hash is valid but whose BVH is not a tree (a self-referencing
+    child) or is deeper than the 64-entry wave stack is rejected on load; the depth is recomputed from
+    the nodes, never trusted from the header."""
+    import struct
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path("cube.obj")), device=rt.RT_DEVICE_NONE)
+    p = tmp_path / "cube.rtscene"
+    sc.save(p)
+    raw = p.read_bytes()
+    sec = _cache_sections(raw)
+    assert _cache_sign(sec) == raw  # the re-signer reproduces the library's hash
+    bad = tmp_path / "crafted.rtscene"
+    # 1. node 0 (the root) lists itself as child 0
+    s1 = [bytearray(x) for x in sec]
+    struct.pack_into("<I", s1[12], 48, 0)
+    bad.write_bytes(_cache_sign(s1))
+    with pytest.raises(rt.RTError, match="not a tree"):
+        rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
+    # 2. a 70-level chain (each node once, so a tree) under a header that claims depth 3
+    n = 70
+    leaf0 = 0x80000000  # leaf handle: triangle 0, count 1
+    chain = bytearray()
+    for i in range(n):
+        rec = bytearray(sec[12][:64])
+        struct.pack_into("<II", rec, 48, i + 1 if i + 1 < n else leaf0, leaf0)
+        chain += rec
+    s2 = [bytearray(x) for x in sec]
+    s2[12] = chain
+    struct.pack_into("<i", s2[0], 36, n)        # n_nodes
+    struct.pack_into("<i", s2[0], 40, 0)        # no wide tree
+    struct.pack_into("<i", s2[0], 52, 3)        # depth (a lie)
+    s2[13] = bytearray()
+    bad.write_bytes(_cache_sign(s2))
+    with pytest.raises(rt.RTError, match="deeper than the traversal stack"):
+        rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
+    # 3. the same chain at 40 levels loads, with its real depth
+    s3 = [bytearray(x) for x in s2]
+    s3[12] = chain[: 40 * 64]
+    struct.pack_into("<II", s3[12], 39 * 64 + 48, leaf0, leaf0)
+    struct.pack_into("<i", s3[0], 36, 40)
+    bad.write_bytes(_cache_sign(s3))
+    assert rt.Scene.load(bad, device=rt.RT_DEVICE_NONE).info()["bvh_depth"] == 41
 
 
 def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
