@@ -2,27 +2,35 @@
 """Benchmark of the MI355X ray-traversal hot path (BASELINE.json metric).
 
 Metric: "Mrays/s (primary) + frame ms at 1920x1080, 1M-tri BVH, 1/2/4/8 GPU".
-Workload (C3): 1,000,000 random triangles (SplitMix64 seed 12345), Flycamera eye
-(0,0,1) (translate(0,0,20)), fovy 60, one white light at (-0.5,2,3), PRIMARY mode (closest hit +
-unshadowed Phong). A step = one frame: one launch of the render kernel over this rank's 16x16 tiles.
-Scene and frame buffer are resident in HBM before the timed region; no host copies inside it.
-
-Multi-GPU (one process per GPU, torchrun): the frame grows with N at 16:9 so that every GPU traces a
-1080p-equivalent share (weak scaling; N=4 is C4's 3840x2160); tiles are interleaved over ranks, the
-scene is replicated, and there is no collective on the data path (barrier + max/sum reductions of the
-timing only). `--frame WxH` fixes the frame instead (strong scaling, e.g. --frame 3840x2160).
+Workloads: 1,000,000 random triangles (SplitMix64 seed 12345), Flycamera eye (0,0,1)
+(translate(0,0,20)), fovy 60, one white light at (-0.5,2,3), PRIMARY mode (closest hit + unshadowed
+Phong). A step = one frame: one launch of the render kernel over this rank's 16x16 tiles. Scene and
+frame buffer are resident in HBM before the timed region; no host copies inside it.
+  N = 1: C3, the 1920x1080 frame on one GPU.
+  N > 1: C4, the 3840x2160 frame split over the N ranks (strong scaling: the frame is fixed; 16x16 tiles
+         interleaved over ranks, scene replicated, no collective on the data path -- barrier + MAX/SUM of
+         the timing only). The line also carries the 1080p frame split the same way ("c3_frame").
+  --frame WxH overrides the frame.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including:
-  roofline: algorithmic bytes per ray B = 64*N_node + 40*N_tri + 92*hit + 12 from a
-            counting run of the same kernel on the same frame, times rays per launch, over the average
-            launch duration measured with HIP events on the library's stream; peak 8 TB/s HBM3E.
+  roofline: HBM roofline of the dominant kernel (k_primary_fused). achieved = the packet algorithm's bytes
+            per launch (64-B node record per wave per visited node, 64-B triangle record per wave per
+            tested triangle -- the counting run's wave fetch counts -- plus per hit lane the 64-B hit
+            triangle record and the 48-B shading record, plus the 12-B pixel) / the kernel's launch
+            duration measured with HIP events with one frame on the GPU; traffic = measured HBM bytes per
+            launch (rocprofv3 FETCH_SIZE/WRITE_SIZE, profiles/pmc_latest.json, only when that profile was
+            taken of this same build and workload) over the same duration; "limiter" and "issue": what
+            actually bounds the kernel per the same profile's SQ counters (VALU / SALU issue fractions at
+            the measured clock, wave cycles spent waiting).
   cpu_baseline: the CPU restatement of the reference algorithm (oracle/, "port") on a bounded pixel
-            sample of the same frame, timed on this host's cores.
+            sample of the same frame on this host's CPU share, with the parity of those pixels against
+            the GPU frame and the calibration of the port against the reference's own measured rate.
 """
 import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -30,6 +38,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "ray-tracing-project_amd")
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+N_CU, SIMD_PER_CU = 256, 4
 
 
 def load_rtamd():
@@ -43,13 +53,37 @@ def load_rtamd():
 def frame_for(n_gpus, override):
     if override:
         w, h = override.lower().split("x")
-        return int(w), int(h), "strong"
-    s = math.sqrt(n_gpus)
-    return 8 * round(1920 * s / 8), 8 * round(1080 * s / 8), "weak"
+        return int(w), int(h)
+    return (1920, 1080) if n_gpus == 1 else (3840, 2160)
 
 
-def cpu_baseline(scene, soup_args, W, H, full, target_s, threads):
-    """Oracle ("port" of the reference algorithm) on a strided pixel sample of the same frame."""
+def shard_tiles(W, H, rank, n):
+    """16x16 tiles this rank renders (the kernel's assignment: tile t goes to rank t % n)."""
+    tx = (W + 15) // 16
+    return [(t % tx, t // tx) for t in range(rank, tx * ((H + 15) // 16), n)]
+
+
+def cpu_threads():
+    """The CPU share this process may use: the GPU box exports OMP_NUM_THREADS=16 per GPU (its machine has
+    far more cores, shared with other jobs); elsewhere every core in the affinity mask."""
+    avail = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(avail, share) if share > 0 else avail), avail
+
+
+def cpu_model():
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(scene, soup_args, W, H, full, target_s, threads, avail, gpu_frame):
+    """Oracle ("port" of the reference algorithm) on a strided pixel sample of the same frame, and the
+    parity of those pixels against the GPU frame (rgb, face, t of the same camera)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     t0 = time.perf_counter()
@@ -69,27 +103,45 @@ def cpu_baseline(scene, soup_args, W, H, full, target_s, threads):
         idx = np.arange(k // 2, W * H, k, dtype=np.int64)
         pix = np.stack([idx % W, idx // W], axis=1).astype(np.int32)
         t = time.perf_counter()
-        sc.render(cam, O.DEFAULT_LIGHTS, W, H, full=full, pixels=pix, threads=threads)
-        return len(pix), time.perf_counter() - t
+        out = sc.render(cam, O.DEFAULT_LIGHTS, W, H, full=full, pixels=pix, threads=threads)
+        return idx, out, time.perf_counter() - t
 
-    n, dt = run(509)  # calibration sample (~4k rays)
+    idx, out, dt = run(509)  # calibration sample (~4k rays)
     k = 509
     for _ in range(3):
-        rate = n / max(dt, 1e-6)
+        rate = len(idx) / max(dt, 1e-6)
         k = max(1, math.ceil(W * H / max(rate * target_s, 1.0)))
-        n, dt = run(k)
+        idx, out, dt = run(k)
         if dt > 0.6 * target_s or k == 1:
             break
-    return {"value": round(n / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{n} primary rays = every {k}th pixel (row-major) of the same {W}x{H} frame "
-                      f"({what}, eye (0,0,1), {'FULL' if full else 'PRIMARY'}); {dt:.1f} s of CPU work on "
-                      f"{threads} threads; box partition build {build_s:.1f} s excluded"}
-
-
-def shard_tiles(W, H, rank, n):
-    """16x16 tiles this rank renders (the kernel's assignment: tile t goes to rank t % n)."""
-    tx = (W + 15) // 16
-    return [(t % tx, t // tx) for t in range(rank, tx * ((H + 15) // 16), n)]
+    n = len(idx)
+    res = {"value": round(n / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": f"{n} primary rays = every {k}th pixel (row-major) of the same {W}x{H} frame "
+                     f"({what}, eye (0,0,1), {'FULL' if full else 'PRIMARY'}); {dt:.1f} s of CPU work on "
+                     f"{threads} threads; box partition build {build_s:.1f} s excluded",
+           "cores_available": avail, "model": cpu_model(),
+           "rays_per_s_per_thread": round(n / dt / threads, 1)}
+    calib = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(calib):
+        c = json.load(open(calib))
+        res["calibration"] = {
+            "port_over_reference": c["port_over_reference"],
+            "how": f"port {c['port_rays_per_s_per_thread']} vs the unmodified reference's "
+                   f"{c['reference_rays_per_s_per_core']} primary rays/s per core, same scene / camera / 32x18 "
+                   f"sample, one thread, both in the survey's container ({c['host']}): profiles/cpu_calibration.json",
+            "reference_equivalent_mrays_per_s": round(n / dt / 1e6 / c["port_over_reference"], 6)}
+    if gpu_frame is not None:
+        grgb, gface, gt = gpu_frame
+        orgb, oface, ot = out
+        gr = grgb.reshape(-1, 3)[idx]
+        err = np.abs(gr.astype(np.float64) - orgb.astype(np.float64))
+        err = np.where(np.isnan(gr) & np.isnan(orgb), 0.0, err)
+        res["parity"] = {"pixels": n, "face_mismatch": int((gface.reshape(-1)[idx] != oface).sum()),
+                         "t_mismatch": int((gt.reshape(-1)[idx].view(np.uint32) != ot.view(np.uint32)).sum()),
+                         "linf": float(np.nanmax(err)) if err.size else 0.0,
+                         "what": "the oracle's sampled pixels vs the same pixels of the GPU frame (face id and t "
+                                 "bits, colour L_inf)"}
+    return res
 
 
 def e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist, iters=5):
@@ -143,24 +195,53 @@ def make_reducer(dist, dev):
     return reduce
 
 
-def measured_traffic(W, H, n_faces, mode, kernel_ms, kernel):
-    """HBM traffic of the same kernel on the same workload from the committed rocprofv3 PMC summary
-    (profiles/pmc_latest.json, tools/profile.sh + tools/summarize_profile.py): 2*FETCH_SIZE + WRITE_SIZE
-    bytes per launch (gfx950 correction), expressed as GB/s over this run's average launch time."""
+def same_build_profile(W, H, n_faces, mode, kernel, src_hash):
+    """The committed rocprofv3 summary (profiles/pmc_latest.json, tools/profile.sh +
+    tools/summarize_profile.py) when it was taken of this build (embedded source hash), this kernel and
+    this workload, one frame on the GPU at a time; else None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
-        return None, None
+        return None, "no profiles/pmc_latest.json"
     d = json.load(open(p))
-    cfg = d.get("bench_line_under_trace", {}).get("config", {})
+    bl = d.get("bench_line_under_trace", {})
+    cfg = bl.get("config", {})
+    why = []
     if cfg.get("frame") != f"{W}x{H}" or cfg.get("triangles") != n_faces or cfg.get("mode") != mode:
-        return None, None
-    if not str(d.get("kernel", "")).startswith(kernel + "<"):  # profiled with another kernel form
-        return None, None
-    b = d.get("hbm_bytes_per_launch")
-    if not b:
-        return None, None
-    return round(b / (kernel_ms * 1e-3) / 1e9, 1), (f"profiles/{d.get('tag')}_pmc.json: "
-                                                   f"{b / 1e6:.1f} MB per launch (2*FETCH_SIZE+WRITE_SIZE)")
+        why.append("other workload")
+    if not str(d.get("kernel", "")).startswith(kernel + "<"):
+        why.append("other kernel")
+    if bl.get("build", {}).get("source_hash") != src_hash:
+        why.append(f"other build ({bl.get('build', {}).get('source_hash')} vs {src_hash})")
+    if why:
+        return None, f"profiles/pmc_latest.json ({d.get('tag')}): " + ", ".join(why)
+    return d, f"profiles/{d.get('tag')}_pmc.json"
+
+
+def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_device):
+    for _ in range(warmup):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    sc.synchronize()
+    barrier()
+    sync_device()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    st = sc.synchronize()
+    sync_device()
+    barrier()
+    return time.perf_counter() - t0, st
+
+
+def isolated_kernel_ms(rt, sc, cam, W, H, mode, shard, iters=20):
+    """The render kernel's launch duration with one frame on the GPU (each frame synchronised before the
+    next is queued): HIP events on the library's stream around each launch, averaged."""
+    tot, trav = 0.0, 0.0
+    for _ in range(iters):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+        st = sc.synchronize()
+        tot += st["kernel_ms"]
+        trav += st["trace_kernel_ms"]
+    return tot / iters, trav / iters
 
 
 def main():
@@ -169,13 +250,14 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tris", type=int, default=1_000_000)
-    ap.add_argument("--frame", default=None, help="WxH (strong scaling); default 1080p per GPU (weak)")
+    ap.add_argument("--frame", default=None, help="WxH; default 1920x1080 on 1 GPU (C3), 3840x2160 split over N>1 (C4)")
     ap.add_argument("--mode", choices=["primary", "full"], default="primary")
     ap.add_argument("--scene", default="soup", help="soup | bunny")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + 8-bit frame to host) timing")
+    ap.add_argument("--no-extra", action="store_true", help="skip the second frame size (c4_frame / c3_frame)")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
     ap.add_argument("--builder", choices=["sah", "lbvh"], default="sah",
                     help="BVH builder: host binned SAH (default) or the device LBVH (SURVEY f2)")
@@ -210,10 +292,15 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def sync_device():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
     reduce = make_reducer(dist, dev)
 
     rt = load_rtamd()
-    W, H, scaling = frame_for(n, a.frame)
+    ident = rt.build_identity()
+    W, H = frame_for(n, a.frame)
     t0 = time.perf_counter()
     if a.scene == "soup":
         mesh, _, _ = rt.soup_mesh(a.tris, 12345)
@@ -230,30 +317,31 @@ def main():
     mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY
     shard = (rank, n)
 
-    for _ in range(a.warmup):
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
-    sc.synchronize()
-
-    barrier()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(a.steps):
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
-    st = sc.synchronize()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-
+    elapsed, st = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device)
     my_rays = st["primary_rays"] * a.steps
     elapsed_max = reduce(elapsed, "MAX")
     total_rays = reduce(float(my_rays), "SUM")
     kernel_ms_avg = st["kernel_ms"] / max(st["launches"], 1)
     kernel_ms_max = reduce(kernel_ms_avg, "MAX")
+    ms_per_step = elapsed_max / a.steps * 1e3
 
-    trace_ms_avg = st["trace_kernel_ms"] / max(st["launches"], 1)
-    trace_ms_max = reduce(trace_ms_avg, "MAX")
+    # the dominant kernel's launch duration with one frame on the GPU (roofline denominator)
+    iso_ms, iso_trace_ms = isolated_kernel_ms(rt, sc, cam, W, H, mode, shard)
+    iso_ms_max = reduce(iso_ms, "MAX")
+
+    # the second frame size: N = 1 -> the C4 frame on this one GPU (strong-scaling base of C4);
+    # N > 1 -> the metric's 1080p frame split over the N ranks
+    extra = None
+    if not a.no_extra and a.frame is None and a.scene == "soup":
+        W2, H2 = (3840, 2160) if n == 1 else (1920, 1080)
+        cam2 = rt.flycam(W2, H2, 0, 0, 20)
+        k2 = max(10, a.steps // 2)
+        el2, st2 = timed_frames(rt, sc, cam2, W2, H2, mode, shard, k2, a.warmup, barrier, sync_device)
+        el2 = reduce(el2, "MAX")
+        rays2 = reduce(float(st2["primary_rays"] * k2), "SUM")
+        extra = {"frame": f"{W2}x{H2}", "workload": "C4 frame on 1 GPU" if n == 1 else f"C3 frame split over {n} GPUs",
+                 "mrays_per_s": round(rays2 / el2 / 1e6, 2), "ms_per_step": round(el2 / k2 * 1e3, 4), "steps": k2}
+
     roof = None
     stats = None
     if rank == 0 and not a.no_stats:
@@ -264,28 +352,39 @@ def main():
         n_node = stats["node_visits"] / rays
         n_tri = stats["tri_tests"] / rays
         hit = stats["hits"] / rays
-        # B = 64 N_node + 40 N_tri + 92 hit + 12 per ray. PRIMARY runs as one kernel
-        # (k_primary_fused: traversal + shading, so its share is the whole B); with RT_KERNEL_VARIANT bit
-        # 32768 it runs as k_trace_primary (64 N_node + 40 N_tri + its 8-B hit record) + k_shade_primary.
-        # FULL: k_render_full carries B (its secondary rays on top are not counted).
         split = mode == rt.RT_MODE_PRIMARY and (int(os.environ.get("RT_KERNEL_VARIANT", "0") or 0) & (32768 | 256 | 2048))
-        b_trace = 64 * n_node + 40 * n_tri + 8
-        b_ray = 64 * n_node + 40 * n_tri + 92 * hit + 12
-        b_kern = b_trace if split else b_ray
-        kern_ms = trace_ms_avg if mode == rt.RT_MODE_PRIMARY else kernel_ms_avg
-        achieved = b_kern * st["primary_rays"] / (kern_ms * 1e-3) / 1e9
         kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
-        traffic, traffic_note = measured_traffic(W, H, info["n_faces"], a.mode, kern_ms, kname)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(achieved / 8000.0, 4), "traffic": traffic, "traffic_source": traffic_note,
-                "kernel": kname,
-                "kernel_ms": round(kern_ms, 4), "bytes_per_ray_kernel": round(b_kern, 1),
-                "bytes_per_ray_path": round(b_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
-                "hit": round(hit, 4),
-                "path_achieved_GBps": round(b_ray * st["primary_rays"] / (kernel_ms_avg * 1e-3) / 1e9, 1),
-                # the same bytes over the wall-clock interval per frame (frames overlap in flight)
-                "achieved_throughput_GBps": round(b_kern * st["primary_rays"] / (elapsed / a.steps) / 1e9, 1),
-                "wave_fetch_bytes_per_ray": round((64 * stats["wave_node_fetches"] + 64 * stats["wave_tri_fetches"]) / rays, 2)}
+        # the packet algorithm's bytes per launch: node / triangle records once per wave, the hit lanes'
+        # triangle + shading records, the pixel
+        wave_bytes = 64.0 * (stats["wave_node_fetches"] + stats["wave_tri_fetches"])
+        alg_bytes = wave_bytes + stats["hits"] * (64 + 48) + 12.0 * rays
+        kern_ms = iso_trace_ms if mode == rt.RT_MODE_PRIMARY else iso_ms
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        prof, prof_src = same_build_profile(W, H, info["n_faces"], a.mode, kname, ident["source_hash"])
+        traffic = traffic_b = issue = limiter = None
+        if prof is not None:
+            traffic_b = prof.get("hbm_bytes_per_launch")
+            if traffic_b:
+                traffic = round(traffic_b / (kern_ms * 1e-3) / 1e9, 1)
+            issue = prof.get("issue")
+            limiter = prof.get("limiter")
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_bytes_per_launch": traffic_b, "traffic_source": prof_src,
+                "kernel": kname, "kernel_ms_isolated": round(kern_ms, 4),
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+                "algorithmic_bytes_per_ray": round(alg_bytes / rays, 1),
+                "per_step_GBps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                "limiter": limiter, "issue": issue,
+                # SURVEY 8(d) d3's per-ray demand (every node / triangle a ray visits, as if each ray read
+                # its own records): served from SGPRs / L2 / MALL, not HBM -- reported, not priced
+                "survey_demand_bytes_per_ray": round(64 * n_node + 40 * n_tri + 92 * hit + 12, 1),
+                "n_node": round(n_node, 2), "n_tri": round(n_tri, 2), "hit": round(hit, 4)}
+
+    gpu_frame = None
+    if rank == 0 and n == 1 and not a.no_cpu:
+        sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
+        gpu_frame = sc.download(W, H, want_hits=True)
 
     e2e = None
     if not a.no_e2e and torch.cuda.is_available():
@@ -293,23 +392,23 @@ def main():
 
     cpu = None
     if rank == 0 and n == 1 and not a.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
+        threads, avail = cpu_threads()
         cpu = cpu_baseline(a.scene, (a.tris, 12345, rt.SOUP_MATERIAL), W, H, a.mode == "full", a.cpu_seconds,
-                           threads)
+                           threads, avail, gpu_frame)
 
     if rank == 0:
         value = total_rays / elapsed_max / 1e6
         if a.scene == "soup":
-            cname = "C3" if (W, H) == (1920, 1080) else ("C4" if (W, H) == (3840, 2160) else "C3-family")
+            cname = "C3" if (W, H) == (1920, 1080) else ("C4" if (W, H) == (3840, 2160) else "soup")
         else:
             cname = "C5" if a.mode == "full" else "C2"
-        extra = {}
+        more = {}
         if e2e is not None:
             # one frame end to end: render + 8-bit frame assembled on rank 0 (RCCL all-gather for N>1) + D2H
-            extra["e2e_frame_ms"] = round(e2e, 3)
+            more["e2e_frame_ms"] = round(e2e, 3)
         if stats is not None:
-            extra["rays_per_frame_total"] = stats["total_rays"]  # primary + shadow + reflection (FULL)
-            extra["total_mrays_per_s"] = round(stats["total_rays"] * n * a.steps / elapsed_max / 1e6, 2)
+            more["rays_per_frame_total"] = stats["total_rays"]  # primary + shadow + reflection (FULL)
+            more["total_mrays_per_s"] = round(stats["total_rays"] * n * a.steps / elapsed_max / 1e6, 2)
         out = {
             "metric": "Mrays/s (primary) + frame ms at 1920x1080, 1M-tri BVH, 1/2/4/8 GPU",
             "value": round(value, 2),
@@ -317,30 +416,33 @@ def main():
             "n_gpus": n,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
+            "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": scaling,
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"{cname}: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light",
+            "config": {"workload": f"{cname}: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light"
+                                   + (f", split over {n} GPUs" if n > 1 else ""),
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
                        "parallelism": f"tiles/{n} (16x16 tiles interleaved over ranks, scene replicated)",
                        "frames_in_flight": info_fif,
-                       # per-frame latency (first kernel start to last kernel end of one frame); with
-                       # frames in flight, frames overlap and ms_per_step is the throughput interval
+                       # per-frame latency with frames in flight (first kernel start to last kernel end of one
+                       # frame; frames overlap, so ms_per_step is the throughput interval) and alone
                        "kernel_ms_per_frame": round(kernel_ms_max, 4),
-                       "trace_kernel_ms": round(trace_ms_max, 4),
-                       "kernel_mrays_per_s": round(total_rays / a.steps / (kernel_ms_max * 1e-3) / 1e6, 2),
+                       "kernel_ms_one_frame_alone": round(iso_ms_max, 4),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
                        "builder": "lbvh-gpu" if info["builder"] == 1 else "sah-host",
                        "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
                                     "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),
-                                    "upload": round(info["upload_ms"], 1)}, **extra},
+                                    "upload": round(info["upload_ms"], 1)}, **more},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "build": ident,
         }
+        if extra is not None:
+            out["c4_frame" if n == 1 else "c3_frame"] = extra
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

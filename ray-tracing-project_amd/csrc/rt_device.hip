@@ -2150,7 +2150,8 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 // reflection hits / the shadow rays of primary hits; 256 = two rays per lane (PRIMARY), 2048 =
 // persistent-threads PRIMARY traversal with per-XCD work counters (4096: without stealing); 32768 =
 // PRIMARY as trace + shade kernels instead of the fused k_primary_fused; 8192 /
-// 16384 = the FULL megakernel's 8-wave / small-scene (5-wave) build regardless of the scene size.
+// 16384 = the FULL megakernel's 8-wave / small-scene (5-wave) build regardless of the scene size;
+// 65536 = the generic traceRay kernel (k_render_depth) also at the modes' own depths.
 // Default: binary nodes + LDS stack, FULL as one kernel (k_render_full) at the occupancy its scene
 // size selects.
 static int pick_trav(const FrameParams& P, int variant) {
@@ -2361,7 +2362,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const int depth = fr->max_depth > 0 ? fr->max_depth : mode_depth;
   P.max_depth = depth;
   P.shadows = fr->mode == RT_MODE_FULL ? 1 : 0;
-  if (grid > 0 && depth != mode_depth) {
+  if (grid > 0 && (depth != mode_depth || (variant & 65536))) {
     // any other recursion limit: the generic traceRay kernel (one 8x8 wave per block)
     const dim3 g(grid * 4), b(64);
     if (stats) { if (hits) hipLaunchKernelGGL((k_render_depth<true, true>), g, b, 0, st, P); else hipLaunchKernelGGL((k_render_depth<true, false>), g, b, 0, st, P); }

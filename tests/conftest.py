@@ -32,6 +32,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the gfx950 kernels)")
 
 
+# Parity summaries the full-frame GPU tests add (printed at the end of the run, so the driver's record of
+# the test tail carries the measured per-frame error, not only a pass count)
+PARITY_REPORT = []
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    if PARITY_REPORT:
+        terminalreporter.write_sep("-", "full-frame parity vs the CPU oracle")
+        for line in PARITY_REPORT:
+            terminalreporter.write_line(line)
+
+
 @pytest.fixture(scope="session")
 def rt():
     rtamd.lib()

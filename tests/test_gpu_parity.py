@@ -206,7 +206,7 @@ def test_stats_counting_run(rt, soup):
 VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-pipeline": 16, "pipeline-lane-refl": 48,
             "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
             "persistent-no-steal": 2048 | 4096, "full-8-waves": 8192, "full-5-waves": 16384,
-            "split-primary": 32768}
+            "split-primary": 32768, "generic-depth-kernel": 65536}
 
 
 @pytest.mark.parametrize("name", sorted(VARIANTS))
@@ -426,45 +426,53 @@ def test_cli_flyscene_mirror(rt, tmp_path):
     assert cache.exists()
 
 
-def _tie_mesh(rt, n, seed):
+def _tie_arrays(n, seed):
     """Faces whose coordinates come from a tiny set incl. -0.0 / +0.0: ties in every min / max, many
     impossible split axes (axis retries) and duplicate faces."""
     rng = np.random.default_rng(seed)
     vals = np.array([-1.0, -0.0, 0.0, 0.25, 1.0], np.float32)
     v = vals[rng.integers(0, len(vals), size=(3 * n, 3))]
     f = np.arange(3 * n, dtype=np.uint32).reshape(-1, 3)
-    return rt.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32))
+    return v, f
 
 
-def _box_case(rt, soup, name):
-    if name == "soup":
-        return soup[0].mesh, 300
-    if name == "ties":
-        return _tie_mesh(rt, 20000, 7), 20
-    if name == "same":  # every face identical: all three axes fail, one box
-        v = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (400, 1))
-        f = np.arange(1200, dtype=np.uint32).reshape(-1, 3)
-        return rt.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32)), 300
+def _box_case(rt, orc, soup, name):
+    """(product mesh, oracle mesh, min_faces) of a box-partition case"""
+    mat = np.array([rt.SOUP_MATERIAL], np.float32)
+    if name in ("soup", "ties", "same"):
+        if name == "soup":
+            v, f = rt.generate_soup(1_000_000), np.arange(3_000_000, dtype=np.uint32).reshape(-1, 3)
+            return soup[0].mesh, orc.Mesh.from_arrays(v, f, mat), 300
+        if name == "ties":
+            v, f = _tie_arrays(20000, 7)
+            mf = 20
+        else:  # every face identical: all three axes fail, one box
+            v = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (400, 1))
+            f = np.arange(1200, dtype=np.uint32).reshape(-1, 3)
+            mf = 300
+        return rt.Mesh.from_arrays(v, f, mat), orc.Mesh.from_arrays(v, f, mat), mf
     scene, mf = name.split(":")
-    return rt.Mesh.load_obj(scene_path(scene + ".obj")), int(mf)
+    return rt.Mesh.load_obj(scene_path(scene + ".obj")), orc.Mesh.load_obj(scene_path(scene + ".obj")), int(mf)
 
 
 @pytest.mark.parametrize("name", ["cube:300", "dodgeColorTest:300", "bunny:300", "bunny:8", "testding:40", "soup",
                                   "ties", "same"])
-def test_gpu_box_partition(rt, soup, name):
-    """f2: generateBoundingBoxes on the device -- the same boxes (bounds bit for bit), the same box order
-    and the same in-box face order as the host restatement (itself pinned to the oracle and the survey's
-    reference box counts), hence the same tie-break ranks."""
-    mesh, mf = _box_case(rt, soup, name)
+def test_gpu_box_partition(rt, orc, soup, name):
+    """f2: generateBoundingBoxes on the device (BoundingBox.cpp:109-161, flyscene.cpp:399-428) -- the
+    oracle's boxes (bounds bit for bit), box order and in-box face order, hence the same tie-break
+    ranks; and the host builder's, too."""
+    mesh, omesh, mf = _box_case(rt, orc, soup, name)
     host = rt.Scene(mesh, min_faces=mf)
     dev = rt.Scene(mesh, min_faces=mf, box_builder=rt.RT_BOXES_GPU)
     ih, idv = host.info(), dev.info()
     assert ih["box_builder"] == rt.RT_BOXES_HOST and idv["box_builder"] == rt.RT_BOXES_GPU
     assert idv["boxes_gpu_ms"] > 0
     hb, db = host.ref_boxes(), dev.ref_boxes()
-    assert ih["n_ref_boxes"] == idv["n_ref_boxes"], (ih["n_ref_boxes"], idv["n_ref_boxes"])
-    for a, b in zip(hb, db):
-        assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), name
+    ob = orc.Scene(omesh, min_faces=mf).boxes()
+    assert idv["n_ref_boxes"] == len(ob[1]), (idv["n_ref_boxes"], len(ob[1]))
+    for a, b, o in zip(hb, db, ob):
+        assert np.asarray(b).tobytes() == np.asarray(o).tobytes(), (name, "device vs oracle")
+        assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (name, "host vs device")
     if name == "same":
         assert idv["n_ref_boxes"] == 1
     if name in ("bunny:300", "ties"):

@@ -32,13 +32,13 @@ def test_tile_partition_is_exact_cover(WH, n):
     assert counts.max() - counts.min() <= 1  # interleaving balances tile counts
 
 
-def test_weak_scaling_frames():
-    for n, (W, H) in {1: (1920, 1080), 4: (3840, 2160)}.items():
-        assert bench.frame_for(n, None)[:2] == (W, H)
-    for n in (2, 8):
-        W, H, kind = bench.frame_for(n, None)
-        assert kind == "weak" and abs(W * H / n / (1920 * 1080) - 1) < 0.01
-    assert bench.frame_for(8, "3840x2160") == (3840, 2160, "strong")
+def test_default_frames_are_baseline_configs():
+    """N = 1: C3's 1920x1080 frame; N > 1: C4's fixed 3840x2160 frame split over the ranks (strong
+    scaling), so every multi-GPU line lands on a BASELINE config."""
+    assert bench.frame_for(1, None) == (1920, 1080)
+    for n in (2, 4, 8):
+        assert bench.frame_for(n, None) == (3840, 2160)
+    assert bench.frame_for(8, "1920x1080") == (1920, 1080)
 
 
 def _free_port():

@@ -29,14 +29,14 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
     shutil.copy(stats_src, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     avg_ns = None
     for r in csv.DictReader(open(stats_src)):
-        if kernel in r["Name"]:
+        if "::" + kernel in r["Name"]:
             avg_ns = float(r["AverageNs"])
     counters = defaultdict(list)
     for d in sorted(os.listdir(prof)):
         f = os.path.join(prof, d, "run_counter_collection.csv")
         if d.startswith("pmc") and os.path.exists(f):
             for r in csv.DictReader(open(f)):
-                if kernel in r["Kernel_Name"]:
+                if "::" + kernel in r["Kernel_Name"]:
                     counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
     mean = {k: sum(v) / len(v) for k, v in counters.items()}
     out = {"kernel": kernel, "avg_kernel_ns_trace": avg_ns, "counters_mean_per_dispatch": mean,
@@ -53,7 +53,7 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
     trace_csv = os.path.join(prof, "trace", "run_kernel_trace.csv")
     bl = out.get("bench_line_under_trace")
     if bl and os.path.exists(trace_csv):
-        rows = [r for r in csv.DictReader(open(trace_csv)) if kernel in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(open(trace_csv)) if "::" + kernel in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         w, k = int(bl["warmup"]), int(bl["steps"])
         d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[w:w + k]]
@@ -68,8 +68,38 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
         out["hbm_write_bytes_per_launch"] = write
         if avg_ns:
             out["hbm_GBps"] = (fetch + write) / avg_ns
+    # Clock and issue roofline. GRBM_GUI_ACTIVE counts busy GPU cycles summed over the 8 XCDs; the
+    # profile is taken with one frame on the GPU at a time (tools/profile.sh: --frames-in-flight 1), so
+    # the trace's kernel duration is the duration the counters saw and GRBM/8 / duration = the clock.
+    # Issue capacity per cycle: one wave64 VALU instruction per 2 cycles per SIMD-32 (4 SIMDs per CU),
+    # one SALU / one SMEM instruction per cycle per CU (MI355X_MICROARCH.md); SQ_WAVE_CYCLES and the
+    # SQ_WAIT / ACTIVE counters are in quad-cycles.
     if "GRBM_GUI_ACTIVE" in mean and avg_ns:
-        out["effective_clock_GHz"] = mean["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+        clk = mean["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+        out["effective_clock_GHz"] = clk
+        cyc = avg_ns * clk
+        issue = {"clock_GHz": round(clk, 3), "kernel_ns": round(avg_ns, 1)}
+        if "SQ_INSTS_VALU" in mean:
+            issue["valu_per_launch"] = mean["SQ_INSTS_VALU"]
+            issue["valu_frac"] = round(mean["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 4)
+        if "SQ_INSTS_SALU" in mean:
+            issue["salu_per_launch"] = mean["SQ_INSTS_SALU"]
+            issue["salu_frac"] = round(mean["SQ_INSTS_SALU"] / (256 * cyc), 4)
+        if "SQ_INSTS_SMEM" in mean:
+            issue["smem_frac"] = round(mean["SQ_INSTS_SMEM"] / (256 * cyc), 4)
+        if "SQ_WAVE_CYCLES" in mean:
+            issue["mean_resident_waves_per_simd"] = round(4 * mean["SQ_WAVE_CYCLES"] / (1024 * cyc), 2)
+            for k, name in (("SQ_WAIT_ANY", "wave_cycles_waiting"), ("SQ_ACTIVE_INST_ANY", "wave_cycles_issuing"),
+                            ("SQ_WAIT_INST_ANY", "wave_cycles_issue_stalled")):
+                if k in mean:
+                    issue[name] = round(mean[k] / mean["SQ_WAVE_CYCLES"], 4)
+        out["issue"] = issue
+        if "valu_frac" in issue and "wave_cycles_waiting" in issue:
+            out["limiter"] = (f"latency: waves wait on memory (s_waitcnt) {100 * issue['wave_cycles_waiting']:.0f}% "
+                              f"of their cycles and issue in {100 * issue.get('wave_cycles_issuing', 0):.0f}%; "
+                              f"VALU issue at {100 * issue['valu_frac']:.0f}% and SALU at "
+                              f"{100 * issue.get('salu_frac', 0):.0f}% of peak; HBM at "
+                              f"{100 * out.get('hbm_bytes_per_launch', 0) / avg_ns / 8000:.1f}% of 8 TB/s")
     if "SQ_WAVE_CYCLES" in mean:
         wc = mean["SQ_WAVE_CYCLES"]
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
