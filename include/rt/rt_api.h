@@ -223,6 +223,8 @@ typedef struct rt_frame {
 
 #define RT_FRAME_WRITE_HITS 1 /* also record per-pixel face index and t (rt_frame_download) */
 #define RT_FRAME_STATS 2      /* counting run: per-ray node visits / triangle tests (slower) */
+#define RT_FRAME_TIMELINE 4   /* diagnostics: each wave of the render kernel records its start / end clocks
+                                 and the CU it ran on (rt_debug_timeline); PRIMARY and FULL kernels */
 
 typedef struct rt_stats {
   double kernel_ms;         /* device time of the render kernels since the previous rt_synchronize,
@@ -328,6 +330,13 @@ int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]);
  * its reflection / secondary-shadow / primary-shadow stages). Every variant renders the same bits.
  * Returns the previous value. */
 int rt_debug_set_variant(int32_t v);
+
+/* Wave timeline of the last frame rendered with RT_FRAME_TIMELINE (diagnostics): per wave, in dispatch
+ * order (workgroup id), 8 words: shader-clock s_memtime at start (lo, hi) and end (lo, hi), the
+ * constant 100 MHz s_memrealtime at start and end (low 32 bits), HW_ID, and XCC_ID << 28 | the logical
+ * wave (tile * 4 + quarter) the block traced. *n_waves = waves of
+ * that frame; capacity_waves smaller than that -> RT_ERR_INVALID. */
+int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64_t* n_waves);
 
 #ifdef __cplusplus
 }

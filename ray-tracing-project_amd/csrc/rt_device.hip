@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -832,6 +833,7 @@ struct WaveLds {
   static constexpr int kEntries = TRAV == TRAV_W4 ? kStack4 : (TRAV == TRAV_LANE ? 1 : 64);
   uint32_t stack[4][kEntries];
   uint64_t mask[4][(STATS && TRAV == TRAV_W4) ? kEntries : 1];
+  uint32_t clk[4];  // one-wave kernels: the wave's start clocks (wave_clock_start), kept out of registers
 };
 
 template <bool ANY, bool STATS, int TRAV>
@@ -944,6 +946,25 @@ __device__ __forceinline__ TriRec64 vload_tri(const TriRec64* base, uint32_t i) 
 }
 
 
+// Light l of the frame, read from the kernel-argument segment. Every kernel takes FrameParams as its
+// first argument, so the lights sit at offsetof(FrameParams, lights) of that segment; indexing them
+// there (scalar loads, l is wave-uniform) means a light loop never makes the compiler copy the whole
+// FrameParams into private memory for a dynamic index -- which it did in the FULL megakernel once the
+// kernel grew (1.7 KB of scratch per lane, 3x slower).
+__device__ __forceinline__ Light frame_light(int l) {
+  typedef const __attribute__((address_space(4))) char* KArg;
+  typedef const __attribute__((address_space(4))) Light* KLight;
+  const KArg base = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
+  const KLight q = (KLight)(base + offsetof(FrameParams, lights) + (size_t)l * sizeof(Light));
+  Light r;
+  for (int k = 0; k < 3; k++) {
+    r.p[k] = q->p[k];
+    r.c[k] = q->c[k];
+  }
+  r.kind = q->kind;
+  return r;
+}
+
 // calculateColor's light direction (flyscene.cpp:607-611): point light -(P - pos).normalized(), or a
 // directional light's stored vector as is
 __device__ __forceinline__ f3 light_dir(f3 p, const Light& l) {
@@ -979,7 +1000,8 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
                                          WaveLds<TRAV, STATS>* lds, int wv, uint32_t* cnt) {
   f3 sum{0.0f, 0.0f, 0.0f};
   for (int l = 0; l < P.n_lights; l++) {
-    const f3 L = light_dir(hi.p, P.lights[l]);
+    const Light lt = frame_light(l);
+    const f3 L = light_dir(hi.p, lt);
     bool blocked = false;
     if (SHADOWS) {
       Ray sr;
@@ -993,7 +1015,7 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       trace_full_ray<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
     }
     f3 c{0.0f, 0.0f, 0.0f};
-    if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
+    if (lane_hit && !blocked) c = phong(P, st, hi, o, L, lt.c);
     sum = f3{sum.x + c.x, sum.y + c.y, sum.z + c.z};
   }
   return f3{clamp01(sum.x), clamp01(sum.y), clamp01(sum.z)};
@@ -1011,6 +1033,9 @@ struct PixelCoord {
   bool active;
 };
 
+#ifndef RT_ORDER_LPT
+#define RT_ORDER_LPT 1
+#endif
 // WPB = waves per block: 4 (one 256-thread block per 16x16 tile) or 1 (one 64-thread block per 8x8
 // quarter, blocks 4t..4t+3 cover tile t; finer-grained dispatch, same pixels and shard assignment)
 template <int WPB = 4>
@@ -1019,7 +1044,13 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   c.lane = threadIdx.x & 63;
   int nb, b;
   int bid = (int)blockIdx.x;
-  if (P.xcd_remap >= 2) {
+  if (RT_ORDER_LPT && WPB == 1 && P.order != nullptr) {
+    // longest-first order from an earlier frame's wave costs (k_order_lpt): a permutation of the
+    // logical waves that keeps each XCD on its own chunked bands; an out-of-range entry (never
+    // produced) falls back to the block's own id, so a wave never leaves the grid
+    const uint32_t o = uniform(P.order[blockIdx.x]);
+    bid = o < gridDim.x ? (int)o : (int)blockIdx.x;
+  } else if (P.xcd_remap >= 2) {
     // chunked XCD order: blocks b and b + 8 share an XCD, so the k-th block of XCD x takes position
     // (k / C) * 8C + x C + k % C -- each XCD receives runs of C consecutive blocks (for one-wave
     // blocks, the four quarters of a tile and its row neighbours) while the runs still interleave
@@ -1070,6 +1101,44 @@ __device__ __forceinline__ Ray primary_ray(const FrameParams& P, int px, int py)
   return r;
 }
 
+// RT_FRAME_TIMELINE: the wave's start / end clocks and where it ran (diagnostics; one uniform branch
+// when off). HW_ID / XCC_ID via s_getreg (hwreg ids 4 and 20, all 32 bits).
+// The start clocks go to the wave's LDS words rather than staying live in registers for the whole
+// kernel (the FULL megakernel's allocation tips into heavy spilling otherwise).
+#ifndef RT_WAVE_CLOCK
+#define RT_WAVE_CLOCK 1
+#endif
+__device__ __forceinline__ void wave_clock_start(const FrameParams& P, uint32_t* clk) {
+  if (RT_WAVE_CLOCK && (P.timeline || P.cost)) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+      clk[0] = (uint32_t)t0;
+      clk[1] = (uint32_t)(t0 >> 32);
+      clk[2] = r0;
+    }
+  }
+}
+__device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint32_t* clk, int lane, int qw) {
+  if (!RT_WAVE_CLOCK || (!P.timeline && !P.cost)) return;
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  struct { uint64_t t0; uint32_t r0; } w;
+  w.t0 = (uint64_t)uniform(clk[0]) | ((uint64_t)uniform(clk[1]) << 32);
+  w.r0 = uniform(clk[2]);
+  if (P.cost && lane == 0) {  // this wave's cost for the next frame's dispatch order
+    const uint64_t dt = t1 - w.t0;
+    P.cost[qw] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+  }
+  if (!P.timeline) return;
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+  if (lane == 0) {
+    uint4* o = reinterpret_cast<uint4*>(P.timeline + 8 * (size_t)blockIdx.x);
+    o[0] = make_uint4((uint32_t)w.t0, (uint32_t)(w.t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+    o[1] = make_uint4(w.r0, r1, hw, (xcc << 28) | ((uint32_t)qw & 0x0FFFFFFFu));
+  }
+}
+
 __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t* cnt, int lane) {
 #pragma unroll
   for (int c = 0; c < ST_COUNT; c++) {
@@ -1077,6 +1146,72 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
     if (c == ST_WNODE || c == ST_WTRI) v = (lane == 0) ? v : 0;  // wave fetches counted once
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(P.stats + c, v);
+  }
+}
+
+// Longest-first dispatch order for the next frame of the same shape (after the frame, one workgroup per
+// XCD class). The default order hands XCD x the dispatch positions p = 8r + x and fills them with the
+// logical waves of class x (below `full`: runs of C consecutive waves, j = (k / C) 8C + x C + k % C for
+// k = p / 8, so an XCD's L2 serves neighbouring tiles; the trailing partial group identity-mapped).
+// This keeps every wave in its class and stably reorders each class by the wave's measured cost,
+// longest first: LPT scheduling -- the waves that finish a frame late become the cheap ones (the
+// measured one-frame tail was 40% of the frame) -- while waves of equal cost keep their spatial order.
+// Counting sort over kLptBuckets log-spaced cost buckets (4 per octave, from the float exponent and two
+// mantissa bits): per-thread counts in LDS, one wave-parallel exclusive scan per bucket, then every
+// thread places its contiguous run of waves. Any order is a permutation: every frame renders identical
+// bits.
+constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
+__device__ __forceinline__ uint32_t lpt_bucket(uint32_t c, int shift) {
+  // 4 buckets per octave: exponent and 2 mantissa bits of (float)c; costs of 2^10 .. 2^18 shader cycles
+  // (0.5 .. 120 us at 2.1 GHz) spread over the buckets, longest first (bucket 0)
+  const int q = (int)(__float_as_uint((float)(c | 1u)) >> 21) - ((127 + 10) << 2);
+  const int b = (q < 0 ? 0 : (q > 4 * 8 - 1 ? 4 * 8 - 1 : q)) >> shift;
+  return (uint32_t)((kLptBuckets >> shift) - 1 - b);
+}
+__global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost, uint32_t* order, int n, int C, int shift) {
+  __shared__ uint32_t cnt[kLptBuckets][kLptThreads];
+  __shared__ uint32_t base[kLptBuckets];
+  const int x = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int full = (n / (8 * C)) * 8 * C;
+  const int m = (n - x + 7) / 8;  // positions 8r + x < n of this class
+  const int chunk = (m + kLptThreads - 1) / kLptThreads, r0 = t * chunk, r1 = min(m, r0 + chunk);
+  const int nb = kLptBuckets >> shift;
+  auto item = [&](int r) {  // the logical wave the default order puts at position 8r + x
+    const int p = 8 * r + x;
+    if (p >= full) return p;
+    const int k = p >> 3;
+    return (k / C) * 8 * C + x * C + (k % C);
+  };
+  uint32_t mine[kLptBuckets];
+  for (int b = 0; b < kLptBuckets; b++) mine[b] = 0;
+  for (int r = r0; r < r1; r++) mine[lpt_bucket(cost[item(r)], shift)]++;
+  for (int b = 0; b < nb; b++) cnt[b][t] = mine[b];
+  __syncthreads();
+  // exclusive scan of each bucket's per-thread counts: wave w scans buckets w, w + 8, ..; lane i owns
+  // threads 8i .. 8i + 7
+  for (int b = wv; b < nb; b += kLptThreads / 64) {
+    uint32_t v[8], s = 0;
+    for (int k = 0; k < 8; k++) { v[k] = cnt[b][8 * lane + k]; s += v[k]; }
+    uint32_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    uint32_t run = incl - s;
+    for (int k = 0; k < 8; k++) { cnt[b][8 * lane + k] = run; run += v[k]; }
+    if (lane == 63) base[b] = incl;  // bucket total
+  }
+  __syncthreads();
+  if (t == 0) {  // bucket totals -> start ranks, longest bucket first
+    uint32_t s = 0;
+    for (int b = 0; b < nb; b++) { const uint32_t v = base[b]; base[b] = s; s += v; }
+  }
+  __syncthreads();
+  for (int b = 0; b < nb; b++) mine[b] = base[b] + cnt[b][t];
+  for (int r = r0; r < r1; r++) {
+    const int j = item(r);
+    const uint32_t rr = mine[lpt_bucket(cost[j], shift)]++;
+    order[8 * rr + x] = (uint32_t)j;
   }
 }
 
@@ -1272,11 +1407,13 @@ template <bool HITS>
 __global__ __launch_bounds__(64 * RT_TRACE_WPB) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
 void k_primary_fused(FrameParams P) {
   __shared__ WaveLds<TRAV_B2_LDS, false> lds;
+  wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<RT_TRACE_WPB>(P);
   const Ray r = primary_ray(P, c.px, c.py);
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
   if (c.active) shade_primary_pixel<HITS>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
+  wave_clock_end(P, lds.clk, c.lane, c.qw);
 }
 
 // FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
@@ -1430,6 +1567,7 @@ template <bool STATS, bool HITS, int TRAV, int WPE = RT_FULL_WAVES_PER_EU>
 __global__ __launch_bounds__(64 * RT_FULL_WPB) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_render_full(FrameParams P) {
   __shared__ WaveLds<TRAV, STATS> lds;
+  wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<RT_FULL_WPB>(P);
   const bool active = c.active;
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
@@ -1452,6 +1590,7 @@ void k_render_full(FrameParams P) {
     }
   }
   if (STATS) flush_stats(P, cnt, c.lane);
+  wave_clock_end(P, lds.clk, c.lane, c.qw);
 }
 
 // traceRay(o, d, 0) for any recursion limit D = P.max_depth (flyscene.cpp:317-371; the reference fixes
@@ -1469,6 +1608,7 @@ template <bool STATS, bool HITS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_FULL_WAVES_PER_EU_SMALL)))
 void k_render_depth(FrameParams P) {
   __shared__ WaveLds<TRAV_B2_LDS, STATS> lds;
+  wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<1>(P);
   const bool active = c.active;
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
@@ -1542,6 +1682,7 @@ void k_render_depth(FrameParams P) {
     }
   }
   if (STATS) flush_stats(P, cnt, c.lane);
+  wave_clock_end(P, lds.clk, c.lane, c.qw);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1672,7 +1813,7 @@ void k_full_shadow(FrameParams P, int pass) {
   uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
   uint32_t bits = 0;
   for (int l = 0; l < P.n_lights; l++) {
-    const f3 Ld = light_dir(p, P.lights[l]);
+    const f3 Ld = light_dir(p, frame_light(l));
     Ray sr;
     sr.o = offset(p, Ld, 0.003f);
     sr.d = Ld;
@@ -1749,10 +1890,11 @@ __device__ __forceinline__ f3 calc_color_bits(const FrameParams& P, MatState& st
                                               uint32_t bits) {
   f3 sum{0.0f, 0.0f, 0.0f};
   for (int l = 0; l < P.n_lights; l++) {
-    const f3 L = light_dir(hi.p, P.lights[l]);
+    const Light lt = frame_light(l);
+    const f3 L = light_dir(hi.p, lt);
     const bool blocked = (bits >> l) & 1u;
     f3 c{0.0f, 0.0f, 0.0f};
-    if (lane_hit && !blocked) c = phong(P, st, hi, o, L, P.lights[l].c);
+    if (lane_hit && !blocked) c = phong(P, st, hi, o, L, lt.c);
     sum = f3{sum.x + c.x, sum.y + c.y, sum.z + c.z};
   }
   return f3{clamp01(sum.x), clamp01(sum.y), clamp01(sum.z)};
@@ -2057,7 +2199,7 @@ void device_release(rt_scene* s) {
     if (b) (void)hipFree(b);
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
-    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue};
+    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline, f.d_cost, f.d_order};
     for (void* b : fb)
       if (b) (void)hipFree(b);
     if (f.stream) (void)hipStreamDestroy((hipStream_t)f.stream);
@@ -2151,7 +2293,10 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 // persistent-threads PRIMARY traversal with per-XCD work counters (4096: without stealing); 32768 =
 // PRIMARY as trace + shade kernels instead of the fused k_primary_fused; 8192 /
 // 16384 = the FULL megakernel's 8-wave / small-scene (5-wave) build regardless of the scene size;
-// 65536 = the generic traceRay kernel (k_render_depth) also at the modes' own depths.
+// 65536 = the generic traceRay kernel (k_render_depth) also at the modes' own depths; 131072 = the
+// default chunked-XCD dispatch order instead of longest-first (k_order_lpt); 262144 = longest-first
+// with half as many cost buckets (2 per octave: coarser, more spatial order kept); 524288 = longest-first
+// also while other frames are in flight.
 // Default: binary nodes + LDS stack, FULL as one kernel (k_render_full) at the occupancy its scene
 // size selects.
 static int pick_trav(const FrameParams& P, int variant) {
@@ -2236,6 +2381,19 @@ static int check_device_scene(rt_scene* s) {
   if (!s) { set_error("null scene"); return RT_ERR_INVALID; }
   if (s->device == RT_DEVICE_NONE) { set_error("scene was created host-only (RT_DEVICE_NONE)"); return RT_ERR_NO_DEVICE; }
   HIPCHECK(hipSetDevice(s->device));
+  return RT_OK;
+}
+
+extern "C" int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64_t* n_waves) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  const rt_scene::FrameSlot& f = s->slots[s->last_slot];
+  if (!(s->last_flags & RT_FRAME_TIMELINE) || !f.d_timeline) { set_error("rt_debug_timeline: last frame had no RT_FRAME_TIMELINE"); return RT_ERR_INVALID; }
+  if (n_waves) *n_waves = s->last_timeline_waves;
+  if (!out8) return RT_OK;
+  if (capacity_waves < s->last_timeline_waves) { set_error("rt_debug_timeline: buffer too small"); return RT_ERR_INVALID; }
+  HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));
+  HIPCHECK(hipMemcpy(out8, f.d_timeline, (size_t)s->last_timeline_waves * 32, hipMemcpyDeviceToHost));
   return RT_OK;
 }
 
@@ -2331,6 +2489,20 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   }
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
+  if (fr->flags & RT_FRAME_TIMELINE) {  // one record per one-wave block of the render kernel
+    const size_t waves = (size_t)grid * 4;
+    if (waves > slot.timeline_waves) {
+      HIPCHECK(hipStreamSynchronize(st));
+      if (slot.d_timeline) (void)hipFree(slot.d_timeline);
+      slot.d_timeline = nullptr;
+      slot.timeline_waves = 0;
+      HIPCHECK(hipMalloc((void**)&slot.d_timeline, waves * 32));
+      slot.timeline_waves = waves;
+    }
+    HIPCHECK(hipMemsetAsync(slot.d_timeline, 0, waves * 32, st));
+    P.timeline = slot.d_timeline;
+    s->last_timeline_waves = (int64_t)waves;
+  }
   if (fr->mode == RT_MODE_FULL && (variant & 16)) {
     // sized by the 16x16-padded frame: every wave of the tile grid has a count slot
     const size_t npad = (size_t)P.tiles_x * 16 * (size_t)P.tiles_y * 16;
@@ -2345,6 +2517,50 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? 64 : sel == 1 ? 4 : sel == 2 ? 16 : 0);
   }
   const int trav = pick_trav(P, variant);
+  // longest-first dispatch (k_order_lpt) for the one-wave render kernels of the default build: this
+  // slot's previous frame of the same shape left its per-wave costs and the order computed from them
+  const int mode_depth0 = fr->mode == RT_MODE_FULL ? 2 : 1;
+  const int depth0 = fr->max_depth > 0 ? fr->max_depth : mode_depth0;
+  const bool one_wave_kernel = !stats && trav == TRAV_B2_LDS &&
+                               ((fr->mode == RT_MODE_PRIMARY && depth0 == 1 && !(variant & (32768 | 256 | 2048 | 65536))) ||
+                                (fr->mode == RT_MODE_FULL && depth0 == 2 && !(variant & (16 | 65536))) ||
+                                depth0 != mode_depth0 || (variant & 65536));
+  // Only for a frame that has the GPU to itself (no other frame of this scene in flight): then the
+  // tail of the frame would leave the GPU idle and longest-first fills it (one frame at a time: C3
+  // +18%, C5 +28%); with frames in flight the next frame fills the tail and the default order's tile
+  // locality is worth more (LPT measured -3..-7% there). Variant 524288 forces it, 131072 disables it.
+  bool alone = true;
+  for (int k = 0; k < s->n_slots; k++)
+    if (k != slot_id && s->slots[k].last_done && hipEventQuery((hipEvent_t)s->slots[k].last_done) == hipErrorNotReady)
+      alone = false;
+  const bool lpt = one_wave_kernel && !(variant & 131072) && P.xcd_remap >= 2 && grid > 0 && (alone || (variant & 524288));
+  bool lpt_sort = false;
+  if (lpt) {
+    const size_t waves = (size_t)grid * 4;
+    if (waves > slot.order_waves) {
+      HIPCHECK(hipStreamSynchronize(st));
+      if (slot.d_cost) (void)hipFree(slot.d_cost);
+      if (slot.d_order) (void)hipFree(slot.d_order);
+      slot.d_cost = slot.d_order = nullptr;
+      slot.order_waves = 0;
+      slot.order_valid = false;
+      HIPCHECK(hipMalloc((void**)&slot.d_cost, waves * 4));
+      HIPCHECK(hipMalloc((void**)&slot.d_order, waves * 4));
+      slot.order_waves = waves;
+    }
+    const int64_t key[8] = {fr->width, fr->height, si, sc, fr->mode, depth0, P.xcd_remap, (int64_t)waves};
+    const bool same = slot.order_valid && memcmp(key, slot.order_key, sizeof key) == 0;
+    if (same) P.order = slot.d_order;
+    // the order is recomputed from this frame's costs after the frame when it is missing or has served
+    // kLptRefresh frames (the sort costs a few microseconds on the frame's stream; a static or slowly
+    // moving camera keeps its cost map)
+    lpt_sort = !same || ++slot.order_age >= kLptRefresh;
+    if (lpt_sort) {
+      memcpy(slot.order_key, key, sizeof key);
+      slot.order_valid = false;  // until this frame's k_order_lpt has been queued
+      P.cost = slot.d_cost;
+    }
+  }
   if (s->ev_used + 3 > s->ev_pool.size()) {
     if (s->ev_pool.size() >= 3 * 2048) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }
     for (int k = 0; k < 3; k++) {
@@ -2409,6 +2625,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     HIPCHECK(hipGetLastError());
   } else {
     HIPCHECK(hipEventRecord(ev_m, st));
+  }
+  if (lpt_sort) {  // the next frame of this shape on this slot dispatches longest-first
+    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)slot.d_cost, slot.d_order,
+                       (int)(grid * 4), P.xcd_remap, (variant & 262144) ? 1 : 0);
+    HIPCHECK(hipGetLastError());
+    slot.order_valid = true;
+    slot.order_age = 0;
   }
   HIPCHECK(hipEventRecord(ev_b, st));
   slot.last_done = ev_b;

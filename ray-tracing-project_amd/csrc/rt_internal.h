@@ -158,6 +158,12 @@ struct FrameParams {
   uint32_t* woff1;
   uint32_t* counters;         // [0] = |list0|, [1] = |list1|
   int32_t n_waves_max;        // list waves of the worst case (every pixel listed)
+  uint32_t* timeline;         // RT_FRAME_TIMELINE: 8 words per wave (rt_debug_timeline), else null
+  // dispatch order of the one-wave render kernels (longest waves first, from an earlier frame's costs):
+  // order[blockIdx] = the logical wave (tile * 4 + quarter) this block traces; null = the default
+  // chunked-XCD order. cost[logical wave] receives the wave's duration in shader cycles (null = off).
+  const uint32_t* order;
+  uint32_t* cost;
 };
 
 // Ray-list query parameters (rt_trace_closest / rt_trace_shadow)

@@ -95,12 +95,23 @@ struct rt_scene {
     size_t full_pixels = 0;
     void* last_done = nullptr;  // event after this slot's latest frame (since the last synchronize)
     uint32_t* d_queue = nullptr;  // persistent-threads variant: 8 per-XCD work counters
+    uint32_t* d_timeline = nullptr;  // RT_FRAME_TIMELINE records (8 words per wave)
+    size_t timeline_waves = 0;
+    // longest-first dispatch order: per-wave costs of this slot's last frame and the order computed
+    // from them for its next frame, valid for frames with the same order_key
+    uint32_t* d_cost = nullptr;
+    uint32_t* d_order = nullptr;
+    size_t order_waves = 0;
+    int64_t order_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool order_valid = false;  // d_order holds an order for frames of order_key
+    int order_age = 0;         // frames dispatched with that order since it was computed
   };
   static constexpr int kMaxSlots = 4;
   FrameSlot slots[kMaxSlots];
   int n_slots = 1, next_slot = 0, last_slot = 0;
   int32_t last_W = 0, last_H = 0, last_flags = 0, last_shard_index = 0, last_shard_count = 1;
   int64_t last_rays = 0, last_total_rays = 0;
+  int64_t last_timeline_waves = 0;  // waves recorded by the last RT_FRAME_TIMELINE frame
   bool pending = false;
 };
 

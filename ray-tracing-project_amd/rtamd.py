@@ -16,6 +16,7 @@ RT_MODE_PRIMARY = 0
 RT_MODE_FULL = 1
 RT_FRAME_WRITE_HITS = 1
 RT_FRAME_STATS = 2
+RT_FRAME_TIMELINE = 4
 RT_DEVICE_NONE = -2
 
 # Every symbol include/rt/rt_api.h declares (checked by tests/test_abi.py)
@@ -29,6 +30,7 @@ EXPORTS = [
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
+    "rt_debug_timeline",
 ]
 
 
@@ -134,6 +136,7 @@ def lib():
         L.rt_debug_math_device.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
+        L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
         L.rt_frame_download_rgb8.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
@@ -308,6 +311,14 @@ class Scene:
         t = np.zeros((H, W), np.float32) if want_hits else None
         check(lib().rt_frame_download(self.h, W * H, _p(rgb), _p(face), _p(t)))
         return (rgb, face, t) if want_hits else rgb
+
+    def timeline(self):
+        """Per-wave records of the last RT_FRAME_TIMELINE frame: uint32 [n_waves, 8] (rt_debug_timeline)."""
+        n = C.c_int64(0)
+        check(lib().rt_debug_timeline(self.h, 0, None, C.byref(n)))
+        out = np.zeros((n.value, 8), np.uint32)
+        check(lib().rt_debug_timeline(self.h, n.value, _p(out), C.byref(n)))
+        return out
 
     def download_rgb8(self, W, H):
         """The last frame as writePPMImage's 8-bit values (device conversion); returns (rgb8, exact)."""

@@ -494,3 +494,37 @@ def test_gpu_box_partition_nonfinite_uses_host(rt):
     except rt.RTError:
         return  # rejected later in scene creation: nothing built on the device either
     assert sc.info()["box_builder"] == rt.RT_BOXES_HOST
+
+
+def test_longest_first_dispatch_order(rt):
+    """The one-wave render kernels dispatch a slot's next frame of the same shape longest-first
+    (k_order_lpt, from the wave costs the previous frame recorded): the dispatch order is a permutation of
+    the frame's waves that keeps each wave on its chunked-XCD position class and differs from the
+    default order, and every frame renders the same bits as with the default order (variant 131072)."""
+    mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
+    sc = rt.Scene(mesh, frames_in_flight=1)
+    for W, H, mode, depth in ((1920, 1080, rt.RT_MODE_PRIMARY, 0), (1000, 563, rt.RT_MODE_FULL, 0),
+                              (640, 360, rt.RT_MODE_FULL, 3)):
+        cam = rt.flycam(W, H, 0, 0, 20)
+        prev = rt.set_variant(131072)
+        try:
+            ref = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True, max_depth=depth)
+        finally:
+            rt.set_variant(prev)
+        orders = []
+        for k in range(3):  # frame 0: default order (no costs yet); frames 1, 2: longest-first
+            got = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True, max_depth=depth,
+                            flags=rt.RT_FRAME_TIMELINE)
+            for a, b in zip(ref[:3], got[:3]):
+                assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (W, H, mode, depth, k)
+            qw = (sc.timeline()[:, 7] & 0x0FFFFFFF).astype(np.int64)
+            assert np.array_equal(np.sort(qw), np.arange(len(qw))), "dispatch order is not a permutation"
+            orders.append(qw)
+        n = len(orders[0])
+        C = 64
+        full = (n // (8 * C)) * 8 * C
+        pos = np.arange(n)
+        cls = np.where(pos < full, (pos // C) % 8, pos % 8)  # class of logical wave j (default order's XCD)
+        for o in orders[1:]:
+            assert not np.array_equal(o, orders[0])          # reordered
+            assert (cls[o] == pos % 8).all()                 # every wave keeps its XCD position class
