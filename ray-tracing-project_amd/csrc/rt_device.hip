@@ -100,6 +100,32 @@ __device__ __forceinline__ Node64 sload_node_pf(const Node64* base, uint32_t h, 
   __builtin_memcpy(&r, &v, 64);
   return r;
 }
+// The same with the prefetch sinks carried from the previous node step ("+s"): this load's own
+// s_waitcnt retires the previous step's prefetches too, so a node step needs no wait of its own (the
+// sinks stay allocated for the whole traversal; traverse_fast waits once at its end). The child
+// offsets land in registers of their own (o0, o1): a previous prefetch may still be in flight into the
+// sinks when they are loaded (scalar loads return out of order).
+__device__ __forceinline__ Node64 sload_node_pf_carry(const Node64* base, uint32_t h, uint32_t& pf0, uint32_t& pf1) {
+  const uint32_t off = node_offset(__builtin_amdgcn_readfirstlane(h));
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  i16v v;
+  uint32_t o0, o1;
+  asm volatile(
+      "s_load_dwordx16 %0, %5, %6\n\t"
+      "s_load_dword %3, %5, %6 offset:0x38\n\t"
+      "s_load_dword %4, %5, %6 offset:0x3c\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_load_dword %1, %5, %3\n\t"
+      "s_load_dword %2, %5, %4"
+      : "=&s"(v), "+&s"(pf0), "+&s"(pf1), "=&s"(o0), "=&s"(o1)
+      : "s"(bs), "s"(off)
+      : "memory");
+  Node64 r;
+  __builtin_memcpy(&r, &v, 64);
+  return r;
+}
 __device__ __forceinline__ TriRec64 sload_tri(const TriRec64* base, uint32_t i) { return sload64(base, i); }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -308,6 +334,9 @@ struct WaveStack {
 #ifndef RT_PREFETCH_PADLOAD  // 1: offsets re-loaded inside the node-load asm (0: tie-ordered separate asm, measured ±0.5%)
 #define RT_PREFETCH_PADLOAD 1
 #endif
+#ifndef RT_PF_CARRY  // 1: prefetch sinks carried to the next node step (no wait at the end of a step)
+#define RT_PF_CARRY 1
+#endif
 // With RT_PREFETCH, Node64::pad0 / pad1 hold the children's record offsets (multiples of 64), so the
 // eight octant order bits travel in their low bits: octants 0-5 in pad0 bits 0-5, octants 6-7 in pad1
 // bits 0-1. A scalar load ignores the two low offset bits and the rest stays inside the 64-B record,
@@ -447,9 +476,14 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
   uint64_t act = ballot(active);  // lanes still tracing: used by the triangle tests only
   float tlim = active ? INFINITY : -1.0f;  // ANY: box-test limit (-1 once the lane is blocked)
   if (!ANY && !active) h.t = -1.0f;
+#if RT_PREFETCH && RT_PF_CARRY
+  uint32_t cpf0 = 0, cpf1 = 0;  // prefetch sinks, live across the traversal
+#endif
   for (;;) {
     while (!is_leaf(node)) {
-#if RT_PREFETCH
+#if RT_PREFETCH && RT_PF_CARRY
+      const Node64 nd = sload_node_pf_carry(P.nodes, node, cpf0, cpf1);
+#elif RT_PREFETCH
       uint32_t pf0, pf1;
 #if RT_PREFETCH_PADLOAD
       const Node64 nd = sload_node_pf(P.nodes, node, pf0, pf1);
@@ -532,7 +566,7 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
         *slot = far;
       }
       node = nxt;
-#if RT_PREFETCH
+#if RT_PREFETCH && !RT_PF_CARRY
       // the prefetch registers stay allocated until their data has landed (the hardware writes them
       // whenever the load returns); the next record load then hits the scalar cache
       asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(pf0), "s"(pf1) : "memory");
@@ -585,6 +619,9 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
     sp--;
     node = uniform(lds_stack[sp]);
   }
+#if RT_PREFETCH && RT_PF_CARRY
+  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(cpf0), "s"(cpf1) : "memory");  // the last prefetches landed
+#endif
   if (!ANY && !active) h.t = INFINITY;
 }
 

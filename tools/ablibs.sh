@@ -1,15 +1,22 @@
 #!/bin/bash
-# A/B of library builds (make ablib TAG=...) on the bench workload (GPU box). LIBS="default noslp ..."
+# A/B of library builds (make ablib TAG=...) on bench workloads (GPU box), interleaved over REPS rounds so
+# that drift hits every build alike. LIBS="default pfc0 ..."; CFGS="soup:primary:1 soup:primary:4 ..."
+# (scene:mode:frames-in-flight). One JSON line per run under gpurun_out/<TAG>/, a summary line each.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/ab
-for rep in 1 2; do
-for tag in ${LIBS:-default}; do
-  if [ "$tag" = default ]; then lib=""; else lib="$PWD/ray-tracing-project_amd/lib/librtamd_$tag.so"; fi
-  RTAMD_LIB=$lib timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu --no-stats ${BENCH_EXTRA:-} \
-      > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err
-  rc=$?
-  python3 -c "import json; d=json.load(open('gpurun_out/ab/$tag.json')); print('$tag', d['value'], 'Mrays/s', d['config']['kernel_ms_per_frame'], 'ms', d['config'].get('trace_kernel_ms'))" 2>/dev/null || echo "$tag rc=$rc"
-  case $rc in 124|134|137|139) exit $rc;; esac
+TAG=${TAG:-ab}
+mkdir -p gpurun_out/$TAG
+for rep in $(seq 1 ${REPS:-2}); do
+for cfg in ${CFGS:-soup:primary:1 soup:primary:4}; do
+  IFS=: read scene mode fif <<< "$cfg"
+  for tag in ${LIBS:-default}; do
+    if [ "$tag" = default ]; then lib=""; else lib="$PWD/ray-tracing-project_amd/lib/librtamd_$tag.so"; fi
+    out=gpurun_out/$TAG/${tag}_${scene}_${mode}_f${fif}_r$rep.json
+    RTAMD_LIB=$lib timeout -k 10 300 python bench.py --scene $scene --mode $mode --frames-in-flight $fif --steps ${STEPS:-50} \
+        --warmup 5 --no-cpu --no-stats --no-e2e --no-extra ${BENCH_EXTRA:-} > $out 2> ${out%.json}.err
+    rc=$?
+    python3 -c "import json; d=json.load(open('$out')); print('$tag $scene $mode fif$fif r$rep', d['value'], d['ms_per_step'], d['config']['kernel_ms_one_frame_alone'])" 2>/dev/null || echo "$tag rc=$rc"
+    case $rc in 0) ;; *) exit $rc;; esac
+  done
 done
 done
