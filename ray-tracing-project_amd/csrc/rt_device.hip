@@ -337,6 +337,9 @@ struct WaveStack {
 #ifndef RT_PF_CARRY  // 1: prefetch sinks carried to the next node step (no wait at the end of a step)
 #define RT_PF_CARRY 1
 #endif
+#ifndef RT_TOS  // 1: the stack top mirrored in a register, refilled from LDS right after a pop (A/B)
+#define RT_TOS 0
+#endif
 // With RT_PREFETCH, Node64::pad0 / pad1 hold the children's record offsets (multiples of 64), so the
 // eight octant order bits travel in their low bits: octants 0-5 in pad0 bits 0-5, octants 6-7 in pad1
 // bits 0-1. A scalar load ignores the two low offset bits and the rest stays inside the 64-B record,
@@ -479,8 +482,10 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
 #if RT_PREFETCH && RT_PF_CARRY
   uint32_t cpf0 = 0, cpf1 = 0;  // prefetch sinks, live across the traversal
 #endif
+  uint32_t tos = 0;  // RT_TOS: lds_stack[sp - 1] while sp > 0
   for (;;) {
     while (!is_leaf(node)) {
+      const int sp_before = sp;
 #if RT_PREFETCH && RT_PF_CARRY
       const Node64 nd = sload_node_pf_carry(P.nodes, node, cpf0, cpf1);
 #elif RT_PREFETCH
@@ -565,6 +570,7 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
             : "scc");
         *slot = far;
       }
+      if (RT_TOS) tos = sp != sp_before ? far : tos;
       node = nxt;
 #if RT_PREFETCH && !RT_PF_CARRY
       // the prefetch registers stay allocated until their data has landed (the hardware writes them
@@ -617,7 +623,14 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
     }
     if (sp == 0) break;
     sp--;
-    node = uniform(lds_stack[sp]);
+    if (RT_TOS) {
+      // the popped handle is already in a register; the new top is read now and is needed only at
+      // the next pop, by when a node or triangle load's wait has retired the read
+      node = uniform(tos);
+      tos = lds_stack[sp > 0 ? sp - 1 : 0];
+    } else {
+      node = uniform(lds_stack[sp]);
+    }
   }
 #if RT_PREFETCH && RT_PF_CARRY
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(cpf0), "s"(cpf1) : "memory");  // the last prefetches landed
@@ -938,9 +951,18 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #ifndef RT_FULL_OCT_PRIMARY
 #define RT_FULL_OCT_PRIMARY 1
 #endif
+// RT_FULL_LANE_K > 0: a secondary packet with at most K active lanes walks per lane (traverse_lane)
+// instead of as a packet (A/B knob)
+#ifndef RT_FULL_LANE_K
+#define RT_FULL_LANE_K 0
+#endif
 template <bool ANY, bool STATS, int TRAV>
 __device__ __forceinline__ void trace_full_ray(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                                WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
+  if (RT_FULL_LANE_K > 0 && TRAV == TRAV_B2_LDS && __popcll(ballot(active)) <= RT_FULL_LANE_K) {
+    traverse_lane<ANY, STATS>(P, r, active, h, found, cnt);
+    return;
+  }
   if (RT_FULL_OCT) trace_oct<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
   else trace<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
 }
