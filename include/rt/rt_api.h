@@ -145,7 +145,7 @@ typedef struct rt_scene_info {
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);
 
 /* Binary scene cache: rt_scene_save writes everything rt_scene_create derived from
- * the mesh (world vertices, unit normals, the reference box partition and its face order, the BVHs and
+ * the mesh (object and world vertices, unit normals, the reference box partition and its face order, the BVHs and
  * triangle records; versioned, with a content hash); rt_scene_load restores it and uploads it without
  * OBJ parsing or any build. The build parameters (min_faces, max_boxes, leaf_size) come from the file;
  * device, frames_in_flight, default_material and background from opts (NULL = defaults). A truncated,
@@ -202,12 +202,16 @@ int32_t rt_lights_spherical(const rt_light* centre, float radius, int32_t n_poin
  * centre), a point (a point used as a direction); kind = RT_LIGHT_DIRECTIONAL. */
 void rt_light_directional(const rt_camera* cam, const float color[3], rt_light* out);
 
-enum { RT_MODE_PRIMARY = 0, RT_MODE_FULL = 1 };
+enum { RT_MODE_PRIMARY = 0, RT_MODE_FULL = 1, RT_MODE_BOX_COLORS = 2 };
 
 typedef struct rt_frame {
   int32_t width, height;
   int32_t mode;        /* RT_MODE_PRIMARY: closest hit + unshadowed Phong (traceRay at depth limit 1);
-                          RT_MODE_FULL: reference traceRay as-is (shadow per light + 1 reflection) */
+                          RT_MODE_FULL: reference traceRay as-is (shadow per light + 1 reflection);
+                          RT_MODE_BOX_COLORS: traceRay with RENDER_BOUNDINGBOX_COLORED_TRIANGLES set
+                          (flyscene.hpp:166, flyscene.cpp:334-348): a hit pixel is the sum of the colours
+                          of every reference box that hasFace() the closest face, unclamped, no shading,
+                          shadows or reflection (a miss: the background); colours: rt_scene_set_box_colors */
   int32_t shard_index; /* this device renders the 16x16 tiles t (row-major over the frame) with
                           t % shard_count == shard_index */
   int32_t shard_count; /* 1 = whole frame */
@@ -216,7 +220,9 @@ typedef struct rt_frame {
                           fixes 2): 0 = the mode's own (PRIMARY 1, FULL 2); 1..RT_MAX_TRACE_DEPTH = trace
                           that many levels (primary hit + max_depth-1 reflection bounces), with shadow rays
                           in FULL mode and without in PRIMARY mode. The FULL/2 and PRIMARY/1 cases run the
-                          tuned kernels; other depths one generic kernel (same arithmetic, same bits). */
+                          tuned kernels; other depths one generic kernel (same arithmetic, same bits).
+                          RT_MODE_BOX_COLORS returns before any reflection, so every depth >= 1 renders
+                          the same frame there (0 and 1..16 accepted, one kernel). */
 } rt_frame;
 
 #define RT_MAX_TRACE_DEPTH 16
@@ -274,6 +280,17 @@ int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device);
 int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t shard_count, int32_t width, int32_t height,
                                 void* frame_device, int32_t device);
 
+/* Box colours of RT_MODE_BOX_COLORS. The reference draws them in generateBoundingBoxes when its
+ * RENDER_BOUNDINGBOX_COLORED_TRIANGLES flag is set (flyscene.cpp:422-427): BoundingBox::setRandomColor
+ * per box in creation order, colour = (rand() / (float)RAND_MAX) x 3 (BoundingBox.cpp:163-165).
+ * rt_box_colors_random reproduces that sequence from rng (NULL = seed 1: a fresh reference process,
+ * whose first rand() calls these are) into out3 [n_boxes][3]. rt_scene_set_box_colors gives the scene
+ * its colours ([n_ref_boxes][3]; NULL = rt_box_colors_random(n_ref_boxes, NULL)); a scene that renders
+ * RT_MODE_BOX_COLORS without them gets the NULL colours. The per-face sums are computed on the device
+ * at the first box-colour frame after the colours change (one pass over faces x boxes). */
+int rt_box_colors_random(int32_t n_boxes, rt_rand_state* rng, float* out3);
+int rt_scene_set_box_colors(rt_scene* s, const float* colors3);
+
 /* calculateMinimumFace (flyscene.cpp:373-396) for n rays on the device: face -1 = miss (t = +inf) */
 int rt_trace_closest(rt_scene* s, int32_t n, const float* origins3, const float* dirs3, int32_t* face,
                      float* t, float* P3);
@@ -304,8 +321,8 @@ int rt_debug_ray(rt_scene* s, const rt_camera* cam, const rt_light* lights, int3
 int rt_device_count(void);       /* 0 when no GPU is visible */
 int rt_version(void);            /* RT_API_VERSION */
 /* "librtamd api <N> gfx950 sources <hash>": the build's identity. rt_source_hash() is the hash alone:
- * SHA-256 (first 16 hex digits) of the product sources this library was built from (csrc/*.hip,
- * *.cpp, *.h and include/rt/rt_api.h, concatenated in sorted path order), so a record can show that
+ * SHA-256 (first 16 hex digits) of the product sources this library was built from (the csrc/ .hip,
+ * .cpp and .h files and include/rt/rt_api.h, concatenated in sorted path order), so a record can show that
  * the binary it ran matches the tree it came from. */
 const char* rt_version_string(void);
 const char* rt_source_hash(void);

@@ -27,7 +27,8 @@ class Camera(C.Structure):
 
 class RenderOpts(C.Structure):
     _fields_ = [("max_depth", C.c_int32), ("shadows", C.c_int32), ("background", C.c_float * 3),
-                ("def_mat", C.c_float * 12), ("dir_lights6", C.c_void_p), ("n_dir_lights", C.c_int32)]
+                ("def_mat", C.c_float * 12), ("dir_lights6", C.c_void_p), ("n_dir_lights", C.c_int32),
+                ("box_colors3", C.c_void_p)]
 
 
 def lib():
@@ -59,6 +60,7 @@ def lib():
         L.orc_closest.argtypes = [vp, C.c_int32, F32P, F32P, I32P, F32P, F32P]
         L.orc_shadow.argtypes = [vp, C.c_int32, F32P, F32P, I32P]
         L.orc_kat.argtypes = [C.c_int32, C.c_int32, F32P, F32P]
+        L.orc_box_colors_glibc.argtypes = [C.c_int32, F32P]
         L.orc_last_error.restype = C.c_char_p
         _lib = L
     return _lib
@@ -169,14 +171,20 @@ class Scene:
         lib().orc_shadow(self.h, len(P), P, L, out)
         return out
 
-    def render(self, cam, lights, W, H, full=False, pixels=None, threads=1, dir_lights=(), max_depth=None):
+    def render(self, cam, lights, W, H, full=False, pixels=None, threads=1, dir_lights=(), max_depth=None,
+               box_colors=None):
         """lights: [(pos3, color3), ...] point lights; dir_lights: [(vector3, color3), ...] directional lights
         (Flyscene::dirLights). max_depth overrides traceRay's recursion limit (flyscene.hpp:142; FULL = 2
-        with shadows, PRIMARY = 1 without). Returns rgb [n,3], face [n], t [n] (n = W*H or len(pixels))."""
+        with shadows, PRIMARY = 1 without). box_colors [nb,3]: RENDER_BOUNDINGBOX_COLORED_TRIANGLES
+        (flyscene.cpp:334-348). Returns rgb [n,3], face [n], t [n] (n = W*H or len(pixels))."""
         opts = RenderOpts()
         lib().orc_render_opts_default(C.byref(opts), 1 if full else 0)
         if max_depth is not None:
             opts.max_depth = max_depth
+        if box_colors is not None:
+            BC = np.ascontiguousarray(box_colors, np.float32).reshape(-1)
+            assert BC.size == 3 * self.box_count()
+            opts.box_colors3 = BC.ctypes.data
         D6 = np.ascontiguousarray(np.array([list(p) + list(c) for p, c in dir_lights], np.float32).reshape(-1))
         opts.dir_lights6 = D6.ctypes.data if len(dir_lights) else None
         opts.n_dir_lights = len(dir_lights)
@@ -211,6 +219,13 @@ def camera_ray(cam, i, j):
     d = np.zeros(3, np.float32)
     lib().orc_camera_ray(C.byref(cam), i, j, o, d)
     return o, d
+
+
+def box_colors_glibc(n):
+    """BoundingBox::setRandomColor for n boxes of a fresh reference process (glibc srand(1) + rand())."""
+    out = np.zeros((n, 3), np.float32)
+    lib().orc_box_colors_glibc(n, out)
+    return out
 
 
 def kat(op, inp, n, out_len):

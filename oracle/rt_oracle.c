@@ -1015,6 +1015,16 @@ static void trace_ray(const tctx* c, mstate* st, const float* o, const float* d,
     else out[0] = out[1] = out[2] = 0.0f;
     return;
   }
+  if (c->opt->box_colors3) {
+    /* RENDER_BOUNDINGBOX_COLORED_TRIANGLES (flyscene.cpp:334-348): color += box->color over every box
+     * (creation order) with box->hasFace(minimum_face); `number` stays 0, so the sum is returned as is */
+    float col[3] = {0.0f, 0.0f, 0.0f};
+    for (int32_t b = 0; b < c->s->nb; b++)
+      if (box_has_face(&c->s->boxes[b], m, f))
+        for (int k = 0; k < 3; k++) col[k] += c->opt->box_colors3[3 * (size_t)b + k];
+    memcpy(out, col, 12);
+    return;
+  }
   float direct[3];
   calc_color(c, st, f, o, P, direct);
   if (m->fm[f] != -1) memcpy(st->ks, m->mats[m->fm[f]].ks, 12);
@@ -1091,6 +1101,11 @@ int orc_render(orc_scene* s, const orc_camera* cam, const float* lights, int32_t
   for (int32_t i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, render_worker, &jobs[i]);
   for (int32_t i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
   return 0;
+}
+
+void orc_box_colors_glibc(int32_t n, float* out3) {
+  srand(1);
+  for (int32_t i = 0; i < 3 * n; i++) out3[i] = rand() / (float)RAND_MAX;
 }
 
 int orc_closest(orc_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t, float* P) {

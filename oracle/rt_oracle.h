@@ -71,6 +71,9 @@ typedef struct orc_render_opts {
   float def_mat[ORC_MAT_FLOATS]; /* Flyscene default ka/kd/ks/shininess/.. (flyscene.hpp:179-184) */
   const float* dir_lights6;      /* Flyscene::dirLights: [n][direction3, colour3] (flyscene.hpp:135) */
   int32_t n_dir_lights;          /* summed after the point lights (calculateColor, flyscene.cpp:610-612) */
+  const float* box_colors3;      /* non-NULL: RENDER_BOUNDINGBOX_COLORED_TRIANGLES (flyscene.hpp:166): a hit's
+                                    colour is the sum of the colours [nb][3] of every box that hasFace() it
+                                    (flyscene.cpp:334-348), unclamped, with no shading or reflection */
 } orc_render_opts;
 
 void orc_render_opts_default(orc_render_opts* o, int32_t full);
@@ -86,6 +89,11 @@ int orc_closest(orc_scene* s, int32_t n, const float* o3, const float* d3, int32
                 float* P3);
 /* shadow(P, L) for n rays: out 1 = blocked */
 int orc_shadow(orc_scene* s, int32_t n, const float* P3, const float* L3, int32_t* out);
+
+/* BoundingBox::setRandomColor for n boxes in creation order (BoundingBox.cpp:163-165, called by
+ * generateBoundingBoxes :422-427): the C library's own srand(1) + rand() (glibc: the sequence of a fresh
+ * reference process), rand() / (float)RAND_MAX per component. Not thread-safe (global rand state). */
+void orc_box_colors_glibc(int32_t n, float* out3);
 
 /* Eigen-order primitive known-answer entry point (op codes as in oracle/eigen_kat.cpp) */
 int orc_kat(int32_t op, int32_t n, const float* in, float* out);

@@ -1,5 +1,5 @@
 // rt_cache.cpp -- binary scene cache: everything rt_scene_create derives from a mesh
-// (world vertices, unit normals, plane distances, the reference's flat box partition with its face
+// (object and world vertices, unit normals, plane distances, the reference's flat box partition with its face
 // order, the traversal BVHs and triangle records), written once and reloaded without OBJ parsing or
 // any build. The file is a versioned little-endian image of HostScene with a 64-bit content hash.
 #include <chrono>
@@ -14,7 +14,7 @@
 namespace {
 
 constexpr char kMagic[8] = {'R', 'T', 'S', 'C', 'E', 'N', 'E', '1'};
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;  // 2: + object-space vertices (RT_MODE_BOX_COLORS)
 
 struct Header {
   char magic[8];
@@ -113,6 +113,7 @@ extern "C" int rt_scene_save(const rt_scene* s, const char* path) {
   Writer w{fp.get()};
   w.put(&h, sizeof h);
   w.vec(hs.wv);
+  w.vec(hs.ov3);
   w.vec(hs.vnn);
   w.vec(hs.fnn);
   w.vec(hs.fdist);
@@ -181,6 +182,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
   memcpy(hs.Minv, h.Minv, sizeof hs.Minv);
   memcpy(hs.MS, h.MS, sizeof hs.MS);
   r.vec(hs.wv, h.nv);
+  r.vec(hs.ov3, 3 * (size_t)h.nv);
   r.vec(hs.vnn, h.nv);
   r.vec(hs.fnn, h.nf);
   r.vec(hs.fdist, h.nf);

@@ -1415,13 +1415,19 @@ void k_trace_primary_x2(FrameParams P) {
 // PRIMARY stage 2: traceRay at depth limit 1 without shadows: calculateColor (flyscene.cpp:603-614)
 // + traceRay's ks update and clamp (:355-370), or the background on a miss (:327-332), for one pixel
 // whose closest hit (t, triangle slot) is known.
-template <bool HITS>
+// BOXCOL: RENDER_BOUNDINGBOX_COLORED_TRIANGLES (flyscene.cpp:334-348) instead of the shading: the hit
+// face's summed box colours (k_face_box_colors), unclamped.
+template <bool HITS, bool BOXCOL = false>
 __device__ __forceinline__ void shade_primary_pixel(const FrameParams& P, const Ray& r, size_t pix, float t,
                                                     uint32_t slot) {
   const bool hit0 = t != INFINITY;
   f3 col;
   int32_t face = -1;
-  if (hit0) {
+  if (BOXCOL && hit0) {
+    face = (int32_t)P.sc.tris[slot].face;
+    const float4 c = reinterpret_cast<const float4*>(P.face_boxcolor)[face];
+    col = f3{c.x, c.y, c.z};
+  } else if (hit0) {
     const TriRec64 tr0 = vload_tri(P.sc.tris, slot);
     HitInfo hi0;
     hi0.face = tr0.face;
@@ -1445,7 +1451,7 @@ __device__ __forceinline__ void shade_primary_pixel(const FrameParams& P, const 
   }
 }
 
-template <bool HITS>
+template <bool HITS, bool BOXCOL>
 __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
   const PixelCoord c = pixel_coord(P);
   if (!c.active) return;
@@ -1454,7 +1460,45 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
   const float t = __uint_as_float(hb.x);
   Ray r;
   if (t != INFINITY) r = primary_ray(P, c.px, c.py);
-  shade_primary_pixel<HITS>(P, r, pix, t, hb.y);
+  shade_primary_pixel<HITS, BOXCOL>(P, r, pix, t, hb.y);
+}
+
+// RT_MODE_BOX_COLORS, once per colour set: for every face id, color += box->color over the reference
+// boxes in creation order whose [low, high] holds all three object-space vertices (BoundingBox::hasFace,
+// BoundingBox.cpp:26-39; flyscene.cpp:337-341), summed in that order in fp32 as the reference does. One
+// thread per face; the boxes (bounds from the refbox array, colours) are staged through LDS in chunks and
+// read as wave-wide broadcasts.
+constexpr int kBoxColorChunk = 1024;
+__global__ __launch_bounds__(256) void k_face_box_colors(const float* fv9, const float* refbox, const float* col3,
+                                                         int nb, int nf, float* out4) {
+  __shared__ float sb[9][kBoxColorChunk];  // low xyz, high xyz, colour rgb
+  const int f = (int)(blockIdx.x * 256u + threadIdx.x);
+  const bool act = f < nf;
+  float v[9];
+  for (int k = 0; k < 9; k++) v[k] = act ? fv9[9 * (size_t)f + k] : 0.0f;
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+  for (int b0 = 0; b0 < nb; b0 += kBoxColorChunk) {
+    const int n = min(kBoxColorChunk, nb - b0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 256) {
+      const float* rb = refbox + 8 * (size_t)(b0 + i);
+      sb[0][i] = rb[0]; sb[1][i] = rb[1]; sb[2][i] = rb[2];
+      sb[3][i] = rb[4]; sb[4][i] = rb[5]; sb[5][i] = rb[6];
+      const float* c = col3 + 3 * (size_t)(b0 + i);
+      sb[6][i] = c[0]; sb[7][i] = c[1]; sb[8][i] = c[2];
+    }
+    __syncthreads();
+    if (act)
+      for (int i = 0; i < n; i++) {
+        bool in = true;
+        for (int k = 0; k < 3; k++) {
+          const float x = v[3 * k], y = v[3 * k + 1], z = v[3 * k + 2];
+          in = in && x >= sb[0][i] && x <= sb[3][i] && y >= sb[1][i] && y <= sb[4][i] && z >= sb[2][i] && z <= sb[5][i];
+        }
+        if (in) { c0 += sb[6][i]; c1 += sb[7][i]; c2 += sb[8][i]; }
+      }
+  }
+  if (act) reinterpret_cast<float4*>(out4)[f] = make_float4(c0, c1, c2, 0.0f);
 }
 
 // PRIMARY as one kernel (default; variant bit 32768 selects the two-kernel form k_trace_primary +
@@ -1462,7 +1506,7 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
 // registers instead of a round trip through HBM, and the traversal state is dead by then, so the
 // shading's registers do not add to the traversal's (64 VGPR, 8 waves/SIMD, a 112-B spill in the
 // shading part). Measured: C3 +2.7% at 4 frames in flight, bunny +4%.
-template <bool HITS>
+template <bool HITS, bool BOXCOL = false>
 __global__ __launch_bounds__(64 * RT_TRACE_WPB) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES_PER_EU)))
 void k_primary_fused(FrameParams P) {
   __shared__ WaveLds<TRAV_B2_LDS, false> lds;
@@ -1471,7 +1515,7 @@ void k_primary_fused(FrameParams P) {
   const Ray r = primary_ray(P, c.px, c.py);
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
-  if (c.active) shade_primary_pixel<HITS>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
+  if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
   wave_clock_end(P, lds.clk, c.lane, c.qw);
 }
 
@@ -2253,7 +2297,8 @@ void device_release(rt_scene* s) {
   (void)hipSetDevice(s->device);
   for (int k = 0; k < s->n_slots; k++)
     if (s->slots[k].stream) (void)hipStreamSynchronize((hipStream_t)s->slots[k].stream);
-  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_refbox, s->d_mats, s->d_stats};  // d_tris: inside d_nodes
+  void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_refbox, s->d_mats, s->d_stats,
+                  s->d_face_boxcolor};  // d_tris: inside d_nodes
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (int k = 0; k < s->n_slots; k++) {
@@ -2267,6 +2312,44 @@ void device_release(rt_scene* s) {
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
   s->ev_pool.clear();
   s->stream = nullptr;
+  s->d_face_boxcolor = nullptr;
+  s->face_boxcolor_valid = false;
+}
+
+// RT_MODE_BOX_COLORS: (re)computes the per-face box-colour sums when the colours changed. The scene's
+// streams are drained first (earlier box-colour frames in flight read the table).
+static int ensure_face_boxcolor(rt_scene* s) {
+  if (s->face_boxcolor_valid) return RT_OK;
+  HostScene& hs = s->hs;
+  if (s->box_colors.size() != 3 * hs.boxes.size()) {
+    const int rc = rt_scene_set_box_colors(s, nullptr);
+    if (rc) return rc;
+  }
+  if (hs.ov3.size() != 3 * (size_t)hs.nv) { set_error("scene has no object-space vertices"); return RT_ERR_INVALID; }
+  for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
+  const size_t nf = (size_t)hs.nf, nb = hs.boxes.size();
+  if (!s->d_face_boxcolor) {
+    HIPCHECK(hipMalloc((void**)&s->d_face_boxcolor, 16 * std::max<size_t>(nf, 1)));
+    s->device_bytes += (int64_t)(16 * std::max<size_t>(nf, 1));
+  }
+  if (nf > 0) {
+    std::vector<float> fv(9 * nf);
+    for (size_t f = 0; f < nf; f++)
+      for (int k = 0; k < 3; k++) memcpy(&fv[9 * f + 3 * k], &hs.ov3[3 * (size_t)hs.fidx[3 * f + k]], 12);
+    float *d_fv = nullptr, *d_col = nullptr;
+    struct Free { float** a; float** b; ~Free() { if (*a) (void)hipFree(*a); if (*b) (void)hipFree(*b); } } free_{&d_fv, &d_col};
+    HIPCHECK(hipMalloc((void**)&d_fv, fv.size() * 4));
+    HIPCHECK(hipMalloc((void**)&d_col, std::max<size_t>(nb, 1) * 12));
+    HIPCHECK(hipMemcpy(d_fv, fv.data(), fv.size() * 4, hipMemcpyHostToDevice));
+    if (nb) HIPCHECK(hipMemcpy(d_col, s->box_colors.data(), nb * 12, hipMemcpyHostToDevice));
+    hipStream_t st = (hipStream_t)s->stream;
+    hipLaunchKernelGGL(k_face_box_colors, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, d_fv, s->d_refbox, d_col,
+                       (int)nb, (int)nf, s->d_face_boxcolor);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(st));
+  }
+  s->face_boxcolor_valid = true;
+  return RT_OK;
 }
 
 static void fill_scene_params(const rt_scene* s, FrameParams& P) {
@@ -2477,7 +2560,10 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     set_error("rt_render: invalid arguments");
     return RT_ERR_INVALID;
   }
-  if (fr->mode != RT_MODE_PRIMARY && fr->mode != RT_MODE_FULL) { set_error("rt_render: bad mode %d", fr->mode); return RT_ERR_INVALID; }
+  if (fr->mode != RT_MODE_PRIMARY && fr->mode != RT_MODE_FULL && fr->mode != RT_MODE_BOX_COLORS) {
+    set_error("rt_render: bad mode %d", fr->mode);
+    return RT_ERR_INVALID;
+  }
   if (fr->max_depth < 0 || fr->max_depth > RT_MAX_TRACE_DEPTH) {
     set_error("rt_render: max_depth %d outside 0..%d", fr->max_depth, RT_MAX_TRACE_DEPTH);
     return RT_ERR_INVALID;
@@ -2486,6 +2572,8 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const int si = fr->shard_index;
   if (si < 0 || si >= sc) { set_error("rt_render: shard %d of %d", si, sc); return RT_ERR_INVALID; }
   const size_t npix = (size_t)fr->width * fr->height;
+  const bool boxcol = fr->mode == RT_MODE_BOX_COLORS;
+  if (boxcol && (rc = ensure_face_boxcolor(s))) return rc;
   // frames in flight: round-robin over the slots; a slot's stream orders its own frames, frames on
   // different slots overlap (tail of one frame with the start of the next)
   const int slot_id = s->next_slot;
@@ -2537,6 +2625,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   P.t_out = slot.d_t;
   P.stats = s->d_stats;
   P.hits = slot.d_hits;
+  P.face_boxcolor = s->d_face_boxcolor;
   hipStream_t st = (hipStream_t)slot.stream;
   const bool stats = (fr->flags & RT_FRAME_STATS) != 0;
   const bool hits = (fr->flags & RT_FRAME_WRITE_HITS) != 0;
@@ -2578,12 +2667,14 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const int trav = pick_trav(P, variant);
   // longest-first dispatch (k_order_lpt) for the one-wave render kernels of the default build: this
   // slot's previous frame of the same shape left its per-wave costs and the order computed from them
+  // box-colour frames return before any reflection: one depth, the PRIMARY kernels' dispatch
+  const bool prim = fr->mode == RT_MODE_PRIMARY || boxcol;
   const int mode_depth0 = fr->mode == RT_MODE_FULL ? 2 : 1;
-  const int depth0 = fr->max_depth > 0 ? fr->max_depth : mode_depth0;
+  const int depth0 = (fr->max_depth > 0 && !boxcol) ? fr->max_depth : mode_depth0;
   const bool one_wave_kernel = !stats && trav == TRAV_B2_LDS &&
-                               ((fr->mode == RT_MODE_PRIMARY && depth0 == 1 && !(variant & (32768 | 256 | 2048 | 65536))) ||
+                               ((prim && depth0 == 1 && !(variant & (32768 | 256 | 2048 | 65536))) ||
                                 (fr->mode == RT_MODE_FULL && depth0 == 2 && !(variant & (16 | 65536))) ||
-                                depth0 != mode_depth0 || (variant & 65536));
+                                (!boxcol && (depth0 != mode_depth0 || (variant & 65536))));
   // Only for a frame that has the GPU to itself (no other frame of this scene in flight): then the
   // tail of the frame would leave the GPU idle and longest-first fills it (one frame at a time: C3
   // +18%, C5 +28%); with frames in flight the next frame fills the tail and the default order's tile
@@ -2634,10 +2725,10 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   s->ev_used += 3;
   HIPCHECK(hipEventRecord(ev_a, st));
   const int mode_depth = fr->mode == RT_MODE_FULL ? 2 : 1;
-  const int depth = fr->max_depth > 0 ? fr->max_depth : mode_depth;
+  const int depth = depth0;
   P.max_depth = depth;
   P.shadows = fr->mode == RT_MODE_FULL ? 1 : 0;
-  if (grid > 0 && (depth != mode_depth || (variant & 65536))) {
+  if (grid > 0 && !boxcol && (depth != mode_depth || (variant & 65536))) {
     // any other recursion limit: the generic traceRay kernel (one 8x8 wave per block)
     const dim3 g(grid * 4), b(64);
     if (stats) { if (hits) hipLaunchKernelGGL((k_render_depth<true, true>), g, b, 0, st, P); else hipLaunchKernelGGL((k_render_depth<true, false>), g, b, 0, st, P); }
@@ -2645,13 +2736,18 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev_m, st));
   } else if (grid > 0) {
-    if (fr->mode == RT_MODE_PRIMARY && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
+    if (prim && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
       const dim3 g(grid * (4 / RT_TRACE_WPB)), b(64 * RT_TRACE_WPB);
-      if (hits) hipLaunchKernelGGL(k_primary_fused<true>, g, b, 0, st, P);
-      else hipLaunchKernelGGL(k_primary_fused<false>, g, b, 0, st, P);
+      if (boxcol) {
+        if (hits) hipLaunchKernelGGL((k_primary_fused<true, true>), g, b, 0, st, P);
+        else hipLaunchKernelGGL((k_primary_fused<false, true>), g, b, 0, st, P);
+      } else {
+        if (hits) hipLaunchKernelGGL(k_primary_fused<true>, g, b, 0, st, P);
+        else hipLaunchKernelGGL(k_primary_fused<false>, g, b, 0, st, P);
+      }
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));
-    } else if (fr->mode == RT_MODE_PRIMARY) {
+    } else if (prim) {
       if (stats) launch_trace<true>(P, grid, st, trav);
       else if ((variant & 256) && trav == TRAV_B2_LDS)
         hipLaunchKernelGGL(k_trace_primary_x2, dim3(2 * grid), dim3(64), 0, st, P);
@@ -2668,8 +2764,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       else launch_trace<false>(P, grid, st, trav);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));
-      if (hits) hipLaunchKernelGGL(k_shade_primary<true>, dim3(grid), dim3(256), 0, st, P);
-      else hipLaunchKernelGGL(k_shade_primary<false>, dim3(grid), dim3(256), 0, st, P);
+      if (boxcol) {
+        if (hits) hipLaunchKernelGGL((k_shade_primary<true, true>), dim3(grid), dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((k_shade_primary<false, true>), dim3(grid), dim3(256), 0, st, P);
+      } else {
+        if (hits) hipLaunchKernelGGL((k_shade_primary<true, false>), dim3(grid), dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((k_shade_primary<false, false>), dim3(grid), dim3(256), 0, st, P);
+      }
     } else if (!(variant & 16)) {  // FULL as one kernel (default); 16 = the stage pipeline
       // occupancy by scene size (k_render_full); variant bits 8192 / 16384 force the 8-wave / small build
       const size_t rec_bytes = (s->hs.nodes.size() + s->hs.tris.size()) * 64;

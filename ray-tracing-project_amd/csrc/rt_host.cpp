@@ -1268,8 +1268,10 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   // hoisted per-vertex / per-face invariants (same expressions as flyscene.cpp:449-450,459,574-577,599)
   hs.wv.resize(hs.nv);
   hs.vnn.resize(hs.nv);
+  hs.ov3.resize(3 * (size_t)hs.nv);
   for (int32_t i = 0; i < hs.nv; i++) {
     const float* v = d->vertices + 4 * (size_t)i;
+    memcpy(&hs.ov3[3 * (size_t)i], v, 12);
     hs.wv[i] = rt::affv3(hs.M, f3{v[0] / v[3], v[1] / v[3], v[2] / v[3]});
     const float* n = d->vertex_normals + 3 * (size_t)i;
     hs.vnn[i] = rt::normalized(f3{n[0], n[1], n[2]});
@@ -1365,6 +1367,28 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->bvh_gpu_ms = s->bvh_gpu_ms;
   o->box_builder = s->box_builder_used;
   o->boxes_gpu_ms = s->boxes_gpu_ms;
+  return RT_OK;
+}
+
+// BoundingBox::setRandomColor (BoundingBox.cpp:163-165) per box in creation order
+extern "C" int rt_box_colors_random(int32_t n_boxes, rt_rand_state* rng, float* out3) {
+  if (n_boxes < 0 || (n_boxes && !out3)) { rt::set_error("rt_box_colors_random: bad arguments"); return RT_ERR_INVALID; }
+  rt_rand_state local;
+  if (!rng) { rt_rand_seed(&local, 1); rng = &local; }
+  for (int64_t i = 0; i < 3 * (int64_t)n_boxes; i++) out3[i] = (float)rt_rand(rng) / (float)2147483647;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_set_box_colors(rt_scene* s, const float* colors3) {
+  if (!s) { rt::set_error("rt_scene_set_box_colors: null scene"); return RT_ERR_INVALID; }
+  const int32_t nb = (int32_t)s->hs.boxes.size();
+  std::vector<float> c(3 * (size_t)nb);
+  if (colors3) memcpy(c.data(), colors3, c.size() * 4);
+  else rt_box_colors_random(nb, nullptr, c.data());
+  // frames in flight may still read the per-face table: it is rebuilt at the next box-colour frame,
+  // after the scene's streams have drained (rt_device.hip: ensure_face_boxcolor)
+  s->box_colors.swap(c);
+  s->face_boxcolor_valid = false;
   return RT_OK;
 }
 

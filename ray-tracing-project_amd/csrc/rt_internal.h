@@ -164,6 +164,7 @@ struct FrameParams {
   // chunked-XCD order. cost[logical wave] receives the wave's duration in shader cycles (null = off).
   const uint32_t* order;
   uint32_t* cost;
+  const float* face_boxcolor;  // RT_MODE_BOX_COLORS: [n_faces][4] summed box colours per face id
 };
 
 // Ray-list query parameters (rt_trace_closest / rt_trace_shadow)

@@ -29,6 +29,7 @@ struct RefBox {
 struct HostScene {
   int32_t nv = 0, nf = 0;
   std::vector<f3> wv;        // world vertices  (M * v)
+  std::vector<float> ov3;    // object-space vertices [nv][3] (Mesh::getVertex, BoundingBox::hasFace)
   std::vector<f3> vnn;       // normalised vertex normals
   std::vector<f3> fnn;       // normalised face normals
   std::vector<float> fdist;  // facenormal.dot(vert0)
@@ -78,6 +79,11 @@ struct rt_scene {
   rt::TriRec64* d_tris = nullptr;
   float* d_fshade = nullptr;  // per-face shading record: three unit vertex normals + material (float4 x 3)
   float* d_refbox = nullptr;
+  // RT_MODE_BOX_COLORS: the boxes' colours and, per face id, the sum of the colours of the boxes that
+  // hasFace() it (float4; computed on the device when the colours changed)
+  std::vector<float> box_colors;  // [n_boxes][3]; empty = not set yet
+  float* d_face_boxcolor = nullptr;
+  bool face_boxcolor_valid = false;
   rt::DevMat* d_mats = nullptr;
   unsigned long long* d_stats = nullptr;
   int64_t device_bytes = 0;

@@ -57,7 +57,9 @@ class Flyscene {
 
   // light sources for ray tracing (flyscene.hpp:132)
   std::vector<std::pair<Vec3, Vec3>> lights;
-  int mode = RT_MODE_FULL;               // the reference traceRay (max_depth 2, shadows)
+  int mode = RT_MODE_FULL;               // the reference traceRay (max_depth 2, shadows); RT_MODE_BOX_COLORS =
+                                         // RENDER_BOUNDINGBOX_COLORED_TRIANGLES (flyscene.hpp:166) with the
+                                         // boxes' setRandomColor colours of a fresh process
   std::string output = "result.ppm";
   std::vector<float> last_image;         // [H][W][3] float frame (kept only when the 8-bit path was inexact)
   std::string cache_path;                // binary scene cache: loaded if present, written after a build

@@ -1,7 +1,7 @@
 // main.cpp -- headless stand-in for the reference's src/main.cpp key-'T' path (main.cpp:68-69):
 // initialize a Flyscene, optionally move the Flycamera, ray trace, write the PPM.
 //   rt_render_cli <scene.obj> [W H] [--primary] [--dz N] [--out result.ppm] [--device D] [--cache file]
-//                 [--lbvh] [--gpu-boxes]
+//                 [--lbvh] [--gpu-boxes] [--box-colors]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -11,7 +11,7 @@
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    fprintf(stderr, "usage: %s scene.obj [W H] [--primary] [--dz N] [--out file.ppm] [--device D] [--cache file] [--lbvh] [--gpu-boxes]\n",
+    fprintf(stderr, "usage: %s scene.obj [W H] [--primary] [--dz N] [--out file.ppm] [--device D] [--cache file] [--lbvh] [--gpu-boxes] [--box-colors]\n",
             argv[0]);
     return 2;
   }
@@ -22,6 +22,7 @@ int main(int argc, char** argv) {
   int pos = 0;
   for (int i = 2; i < argc; i++) {
     if (!strcmp(argv[i], "--primary")) mode = RT_MODE_PRIMARY;
+    else if (!strcmp(argv[i], "--box-colors")) mode = RT_MODE_BOX_COLORS;
     else if (!strcmp(argv[i], "--dz") && i + 1 < argc) dz = (float)atof(argv[++i]);
     else if (!strcmp(argv[i], "--out") && i + 1 < argc) out = argv[++i];
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(HERE, "lib", "librtamd.so
 
 RT_MODE_PRIMARY = 0
 RT_MODE_FULL = 1
+RT_MODE_BOX_COLORS = 2  # RENDER_BOUNDINGBOX_COLORED_TRIANGLES (flyscene.hpp:166, flyscene.cpp:334-348)
 RT_FRAME_WRITE_HITS = 1
 RT_FRAME_STATS = 2
 RT_FRAME_TIMELINE = 4
@@ -30,7 +31,7 @@ EXPORTS = [
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
-    "rt_debug_timeline",
+    "rt_debug_timeline", "rt_box_colors_random", "rt_scene_set_box_colors",
 ]
 
 
@@ -157,6 +158,8 @@ def lib():
         L.rt_frame_pack_shard_rgb8.argtypes = [vp, vp]
         L.rt_frame_unpack_shards_rgb8.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32]
         L.rt_scene_load.argtypes = [C.c_char_p, C.POINTER(SceneOpts), C.POINTER(vp)]
+        L.rt_box_colors_random.argtypes = [C.c_int32, C.POINTER(RandState), vp]
+        L.rt_scene_set_box_colors.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -387,6 +390,14 @@ class Scene:
         out["ok"] = rc == 0
         return out
 
+    def set_box_colors(self, colors=None):
+        """rt_scene_set_box_colors: colours [n_ref_boxes, 3] of RT_MODE_BOX_COLORS (None = the reference's
+        setRandomColor sequence of a fresh process)."""
+        c = None if colors is None else np.ascontiguousarray(colors, np.float32).reshape(-1, 3)
+        if c is not None and len(c) != self.info()["n_ref_boxes"]:
+            raise ValueError("one colour per reference box")
+        check(lib().rt_scene_set_box_colors(self.h, _p(c)))
+
     def ref_boxes(self):
         inf = self.info()
         nb, nf = inf["n_ref_boxes"], inf["n_faces"]
@@ -487,6 +498,13 @@ class Rand:
 
     def __call__(self):
         return lib().rt_rand(C.byref(self.st))
+
+
+def box_colors_random(n_boxes, rng=None):
+    """BoundingBox::setRandomColor for n_boxes boxes in creation order from rng (None = seed 1)."""
+    out = np.zeros((n_boxes, 3), np.float32)
+    check(lib().rt_box_colors_random(n_boxes, C.byref(rng.st) if rng else None, _p(out)))
+    return out
 
 
 def spherical_light(pos, color, radius, n_points, rng=None):

@@ -528,3 +528,43 @@ def test_longest_first_dispatch_order(rt):
         for o in orders[1:]:
             assert not np.array_equal(o, orders[0])          # reordered
             assert (cls[o] == pos % 8).all()                 # every wave keeps its XCD position class
+
+
+@pytest.mark.parametrize("name", ["cube", "dodgeColorTest", "bunny", "soup"])
+def test_box_colors_mode(rt, orc, soup, name):
+    """RT_MODE_BOX_COLORS = traceRay with RENDER_BOUNDINGBOX_COLORED_TRIANGLES set (flyscene.cpp:334-348):
+    every pixel's colour bit-identical to the oracle's (sum of the colours of the boxes that hasFace() the
+    hit face, in box order), with the reference's setRandomColor colours and with caller-set colours;
+    the fused kernel, the trace + shade pair, a counting frame and any max_depth render the same bits."""
+    if name == "soup":
+        sc, osc = soup
+        W, H, dz = 480, 270, 20
+    else:
+        sc = rt.Scene(rt.Mesh.load_obj(scene_path(name + ".obj")))
+        osc = orc.Scene(orc.Mesh.load_obj(scene_path(name + ".obj")))
+        W, H, dz = (320, 180, 20) if name == "bunny" else (256, 144, 0)
+    nb = osc.box_count()
+    assert sc.info()["n_ref_boxes"] == nb
+    rng = np.random.default_rng(5)
+    for colors in (None, rng.uniform(0, 1, (nb, 3)).astype(np.float32)):
+        if colors is not None:
+            sc.set_box_colors(colors)
+        ocol = orc.box_colors_glibc(nb) if colors is None else colors
+        cam = rt.flycam(W, H, 0, 0, dz)
+        rgb, face, t, st = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_BOX_COLORS, want_hits=True)
+        orgb, oface, ot = osc.render(orc.flycam(W, H, 0, 0, dz), orc.DEFAULT_LIGHTS, W, H, box_colors=ocol,
+                                     threads=16)
+        assert (face.reshape(-1) == oface).all(), name
+        assert same_bits(t.reshape(-1), ot).all(), name
+        assert rgb.reshape(-1, 3).tobytes() == orgb.tobytes(), f"{name}: colours differ from the oracle"
+        assert (face >= 0).any()
+        for kw in (dict(max_depth=3), dict(flags=rt.RT_FRAME_STATS)):
+            got = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_BOX_COLORS, want_hits=True, **kw)
+            assert got[0].tobytes() == rgb.tobytes() and got[1].tobytes() == face.tobytes(), kw
+        prev = rt.set_variant(32768)
+        try:
+            got = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_BOX_COLORS, want_hits=True)
+        finally:
+            rt.set_variant(prev)
+        assert got[0].tobytes() == rgb.tobytes()
+    sc.set_box_colors()  # the shared soup scene goes back to the default colours

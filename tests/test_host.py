@@ -247,12 +247,17 @@ def test_scene_cache_roundtrip(rt, tmp_path, name):
             rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
 
 
+# cache sections (version 2): header, wv, ov3, vnn, fnn, fdist, fidx, fmat, mats, boxes, box faces,
+# face_rank, face_box, nodes, nodes4, tris
+NODES = 13
+
+
 def _cache_sections(raw):
     """Split a scene cache (rt_cache.cpp) into its written chunks: header, then the arrays in write order."""
     import struct
     nv, nf, nm, nb, nbf, nn, nn4, nt = struct.unpack_from("<8i", raw, 16)
     assert struct.unpack_from("<I", raw, 12)[0] == 256
-    sizes = [256, 12 * nv, 12 * nv, 12 * nf, 4 * nf, 12 * nf, 4 * nf, 48 * nm, 44 * nb, 4 * nbf, 4 * nf, 4 * nf,
+    sizes = [256, 12 * nv, 12 * nv, 12 * nv, 12 * nf, 4 * nf, 12 * nf, 4 * nf, 48 * nm, 44 * nb, 4 * nbf, 4 * nf, 4 * nf,
              64 * nn, 64 * nn4, 64 * nt]
     out, off = [], 0
     for n in sizes:
@@ -294,7 +299,7 @@ def test_scene_cache_rejects_crafted_trees(rt, tmp_path):
     bad = tmp_path / "crafted.rtscene"
     # 1. node 0 (the root) lists itself as child 0
     s1 = [bytearray(x) for x in sec]
-    struct.pack_into("<I", s1[12], 48, 0)
+    struct.pack_into("<I", s1[NODES], 48, 0)
     bad.write_bytes(_cache_sign(s1))
     with pytest.raises(rt.RTError, match="not a tree"):
         rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
@@ -303,22 +308,22 @@ def test_scene_cache_rejects_crafted_trees(rt, tmp_path):
     leaf0 = 0x80000000  # leaf handle: triangle 0, count 1
     chain = bytearray()
     for i in range(n):
-        rec = bytearray(sec[12][:64])
+        rec = bytearray(sec[NODES][:64])
         struct.pack_into("<II", rec, 48, i + 1 if i + 1 < n else leaf0, leaf0)
         chain += rec
     s2 = [bytearray(x) for x in sec]
-    s2[12] = chain
+    s2[NODES] = chain
     struct.pack_into("<i", s2[0], 36, n)        # n_nodes
     struct.pack_into("<i", s2[0], 40, 0)        # no wide tree
     struct.pack_into("<i", s2[0], 52, 3)        # depth (a lie)
-    s2[13] = bytearray()
+    s2[NODES + 1] = bytearray()
     bad.write_bytes(_cache_sign(s2))
     with pytest.raises(rt.RTError, match="deeper than the traversal stack"):
         rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
     # 3. the same chain at 40 levels loads, with its real depth
     s3 = [bytearray(x) for x in s2]
-    s3[12] = chain[: 40 * 64]
-    struct.pack_into("<II", s3[12], 39 * 64 + 48, leaf0, leaf0)
+    s3[NODES] = chain[: 40 * 64]
+    struct.pack_into("<II", s3[NODES], 39 * 64 + 48, leaf0, leaf0)
     struct.pack_into("<i", s3[0], 36, 40)
     bad.write_bytes(_cache_sign(s3))
     assert rt.Scene.load(bad, device=rt.RT_DEVICE_NONE).info()["bvh_depth"] == 41
@@ -334,6 +339,29 @@ def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
     v = np.minimum(255, (np.float32(255) * rgb).astype(np.int64)).astype(np.uint8)
     rt.write_ppm_rgb8(b, v)
     assert a.read_bytes() == b.read_bytes()
+
+
+def test_box_colors_random_matches_glibc(rt, orc):
+    """RENDER_BOUNDINGBOX_COLORED_TRIANGLES colours: setRandomColor per box in creation order
+    (BoundingBox.cpp:163-165) = rand() / (float)RAND_MAX from the C library's own srand(1) + rand()."""
+    got = rt.box_colors_random(4480)
+    assert got.tobytes() == orc.box_colors_glibc(4480).tobytes()
+    r = rt.Rand(7)
+    a = rt.box_colors_random(10, r)
+    b = rt.box_colors_random(10, r)  # the state advances: 30 rand() calls per 10 boxes
+    r2 = rt.Rand(7)
+    seq = np.array([r2() for _ in range(60)], np.float32) / np.float32(2147483647)
+    assert np.concatenate([a, b]).reshape(-1).tobytes() == seq.tobytes()
+
+
+def test_scene_box_colors_arguments(rt):
+    sc = rt.Scene(rt.Mesh.load_obj(scene_path("dodgeColorTest.obj")), device=rt.RT_DEVICE_NONE)
+    nb = sc.info()["n_ref_boxes"]
+    sc.set_box_colors()
+    sc.set_box_colors(np.ones((nb, 3), np.float32))
+    with pytest.raises(ValueError):
+        sc.set_box_colors(np.ones((nb + 1, 3), np.float32))
+    assert rt.lib().rt_scene_set_box_colors(None, None) == -1
 
 
 def test_rand_matches_glibc(rt):
