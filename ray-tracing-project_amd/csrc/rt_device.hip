@@ -470,6 +470,16 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kPopMarker = 0xFFFFFFFFu;
 
+#ifndef RT_EARLY_PUSH
+#define RT_EARLY_PUSH 1
+#endif
+// the fast loop's wave-stack push as inline asm: a ds_write issued where it stands (the compiler would
+// otherwise schedule the store with the decision block at the end of the step)
+__device__ __forceinline__ void lds_push(uint32_t* slot, uint32_t v) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)slot;
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
 template <bool ANY, int OCT>
 __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                               uint32_t* lds_stack) {
@@ -504,6 +514,22 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
 #else
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
 #endif
+      // RT_EARLY_PUSH (octant loops): when both children are needed the far one is fixed by the node's
+      // order bit for this octant alone, so it is chosen and pushed the moment the node has arrived --
+      // the LDS write completes under the box tests instead of delaying the next node fetch (the loop
+      // head's s_waitcnt lgkmcnt(0) drains it), and the post-mask decision chain is 9 SALU, not 12
+      uint32_t nearb = 0, farb = 0;
+      if (RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
+        sp = (int)uniform((uint32_t)sp);
+        asm("s_bitcmp1_b32 %[bits], %[oct]\n\t"
+            "s_cselect_b32 %[nb], %[c1], %[c0]\n\t"
+            "s_cselect_b32 %[fb], %[c0], %[c1]"
+            : [nb] "=&s"(nearb), [fb] "=&s"(farb)
+            : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [c0] "s"(uniform(nd.child0)),
+              [c1] "s"(uniform(nd.child1))
+            : "scc");
+        lds_push(lds_stack + sp, farb);
+      }
       const float tcut = ANY ? tlim : h.t;
       const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
       const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
@@ -524,7 +550,24 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
 #else
       uint32_t* const slot = lds_stack + sp;
 #endif
-      if (RT_ORDER_BITS && OCT >= 0) {
+      if (RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
+        // both needed: the near child chosen above; one needed: that one; none: the pop marker
+        asm("s_cmp_lg_u64 %[m1], 0\n\t"
+            "s_cselect_b32 %[nxt], %[nb], %[c0]\n\t"
+            "s_cmp_eq_u64 %[m0], 0\n\t"
+            "s_cselect_b32 %[nxt], %[c1], %[nxt]\n\t"
+            "s_cselect_b64 %[tt], 0, %[m1]\n\t"
+            "s_cmp_lg_u64 %[tt], 0\n\t"
+            "s_addc_u32 %[sp], %[sp], 0\n\t"
+            "s_or_b64 %[tt], %[m0], %[m1]\n\t"
+            "s_cselect_b32 %[nxt], %[nxt], -1"
+            : [nxt] "=&s"(nxt), [sp] "+s"(sp), [tt] "=&s"(tt)
+            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [nb] "s"(nearb)
+            : "scc");
+        far = farb;
+        (void)ta;
+        (void)tb;
+      } else if (RT_ORDER_BITS && OCT >= 0) {
         // near child from the node's order bit for this octant (Node64::pad0), overridden when only
         // one child is needed
         asm("s_cmp_lg_u64 %[m1], 0\n\t"
@@ -2738,12 +2781,15 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   } else if (grid > 0) {
     if (prim && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
       const dim3 g(grid * (4 / RT_TRACE_WPB)), b(64 * RT_TRACE_WPB);
+      // RT_LDS_PAD (diagnostics): extra dynamic LDS per block, to cap the resident waves per CU in
+      // occupancy experiments (160 KiB / (pad + 1 KiB) blocks per CU)
+      static const unsigned lds_pad = [] { const char* e = getenv("RT_LDS_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
       if (boxcol) {
-        if (hits) hipLaunchKernelGGL((k_primary_fused<true, true>), g, b, 0, st, P);
-        else hipLaunchKernelGGL((k_primary_fused<false, true>), g, b, 0, st, P);
+        if (hits) hipLaunchKernelGGL((k_primary_fused<true, true>), g, b, lds_pad, st, P);
+        else hipLaunchKernelGGL((k_primary_fused<false, true>), g, b, lds_pad, st, P);
       } else {
-        if (hits) hipLaunchKernelGGL(k_primary_fused<true>, g, b, 0, st, P);
-        else hipLaunchKernelGGL(k_primary_fused<false>, g, b, 0, st, P);
+        if (hits) hipLaunchKernelGGL(k_primary_fused<true>, g, b, lds_pad, st, P);
+        else hipLaunchKernelGGL(k_primary_fused<false>, g, b, lds_pad, st, P);
       }
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));
