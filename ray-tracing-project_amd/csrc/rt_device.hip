@@ -480,12 +480,11 @@ __device__ __forceinline__ void lds_push(uint32_t* slot, uint32_t v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
 
+// traverse_fast from a given state (node handle, stack depth): the whole traversal starts at the root
+// with an empty stack; the dual-chain loop (traverse_dual) hands over a half-finished one
 template <bool ANY, int OCT>
-__device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
-                                              uint32_t* lds_stack) {
-  if (P.n_nodes == 0) return;
-  int sp = 0;
-  uint32_t node = P.root;
+__device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                                   uint32_t* lds_stack, uint32_t node, int sp) {
   uint64_t act = ballot(active);  // lanes still tracing: used by the triangle tests only
   float tlim = active ? INFINITY : -1.0f;  // ANY: box-test limit (-1 once the lane is blocked)
   if (!ANY && !active) h.t = -1.0f;
@@ -679,6 +678,149 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(cpf0), "s"(cpf1) : "memory");  // the last prefetches landed
 #endif
   if (!ANY && !active) h.t = INFINITY;
+}
+
+template <bool ANY, int OCT>
+__device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                              uint32_t* lds_stack) {
+  if (P.n_nodes == 0) return;
+  traverse_fast_from<ANY, OCT>(P, r, active, h, found, lds_stack, P.root, 0);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dual-chain traversal (PRIMARY, closest hit): one wave walks the BVH for TWO independent 8x8 packets
+// at once -- two node handles, two LDS stacks, two rays per lane. Each node step fetches both packets'
+// records with one wait and then runs both box tests and decisions, so the two dependent fetch ->
+// test -> decide chains overlap inside the wave: the kernel is latency bound (throughput still grows
+// with every extra resident wave at 8 per SIMD), and this doubles the chains in flight per wave slot.
+// Leaves are tested per packet; once one packet's walk ends the other finishes alone (traverse_fast_from).
+// Each packet visits exactly the nodes and triangles of its single-chain walk, in the same order, so
+// the hits are identical bit for bit.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kChainDone = 0xFFFFFFFEu;  // leaf-flagged: ends the dual node loop for that chain
+
+__device__ __forceinline__ void sload_node2(const Node64* base, uint32_t ha, uint32_t hb, Node64& a, Node64& b) {
+  const uint32_t offa = node_offset(__builtin_amdgcn_readfirstlane(ha));
+  const uint32_t offb = node_offset(__builtin_amdgcn_readfirstlane(hb));
+  const uint64_t bp = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bp);
+  i16v va, vb;
+  asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(va), "=&s"(vb)
+               : "s"(bs), "s"(offa), "s"(offb)
+               : "memory");
+  __builtin_memcpy(&a, &va, 64);
+  __builtin_memcpy(&b, &vb, 64);
+}
+
+// one octant-loop node step of a chain whose record has arrived: early push of the far child, both
+// slab tests, the 9-SALU decision (as traverse_fast); returns the next handle (kPopMarker: pop)
+template <int OCT>
+__device__ __forceinline__ uint32_t chain_step(const Node64& nd, const Ray& r, float tcut, int& sp, uint32_t* stack) {
+  sp = (int)uniform((uint32_t)sp);
+  const uint32_t c0 = uniform(nd.child0), c1 = uniform(nd.child1);
+  uint32_t nearb, farb, nxt;
+  uint64_t tt;
+  asm("s_bitcmp1_b32 %[bits], %[oct]\n\t"
+      "s_cselect_b32 %[nb], %[c1], %[c0]\n\t"
+      "s_cselect_b32 %[fb], %[c0], %[c1]"
+      : [nb] "=&s"(nearb), [fb] "=&s"(farb)
+      : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [c0] "s"(c0), [c1] "s"(c1)
+      : "scc");
+  lds_push(stack + sp, farb);
+  const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
+  const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+  const uint64_t m0 = mask_le(s0.tmin, s0.tmax), m1 = mask_le(s1.tmin, s1.tmax);
+  asm("s_cmp_lg_u64 %[m1], 0\n\t"
+      "s_cselect_b32 %[nxt], %[nb], %[c0]\n\t"
+      "s_cmp_eq_u64 %[m0], 0\n\t"
+      "s_cselect_b32 %[nxt], %[c1], %[nxt]\n\t"
+      "s_cselect_b64 %[tt], 0, %[m1]\n\t"
+      "s_cmp_lg_u64 %[tt], 0\n\t"
+      "s_addc_u32 %[sp], %[sp], 0\n\t"
+      "s_or_b64 %[tt], %[m0], %[m1]\n\t"
+      "s_cselect_b32 %[nxt], %[nxt], -1"
+      : [nxt] "=&s"(nxt), [sp] "+s"(sp), [tt] "=&s"(tt)
+      : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [nb] "s"(nearb)
+      : "scc");
+  return nxt;
+}
+
+// a chain that left the dual node loop at a leaf or the pop marker: its triangles, then its pop
+__device__ __forceinline__ void chain_leaf(const DevScene& P, const Ray& r, uint64_t act, Hit& h, uint32_t& node,
+                                           int& sp, const uint32_t* stack) {
+  if (node == kChainDone || !is_leaf(node)) return;
+  bool dummy = false;
+  if (node != kPopMarker) {
+    const uint32_t first = leaf_first(node), count = leaf_count(node);
+    for (uint32_t k = 0; k < count; k++) {
+      const TriRec64 tr = sload_tri(P.tris, first + k);
+      test_tri<false>(P, tr, first + k, r, act, h, dummy);
+    }
+  }
+  if (sp == 0) {
+    node = kChainDone;
+  } else {
+    sp--;
+    node = uniform(stack[sp]);
+  }
+}
+
+template <int OCT>
+__device__ __forceinline__ void traverse_dual(const DevScene& P, const Ray& ra, const Ray& rb, bool acta, bool actb,
+                                              Hit& ha, Hit& hb, uint32_t* sta, uint32_t* stb) {
+  if (P.n_nodes == 0) return;
+  const uint64_t ma = ballot(acta), mb = ballot(actb);
+  if (!acta) ha.t = -1.0f;  // lanes without a ray: neutral (no box passes tmin <= -1)
+  if (!actb) hb.t = -1.0f;
+  uint32_t na = ma ? P.root : kChainDone, nb = mb ? P.root : kChainDone;
+  int spa = 0, spb = 0;
+  for (;;) {
+    while (!is_leaf(na) && !is_leaf(nb)) {
+      Node64 a, b;
+      sload_node2(P.nodes, na, nb, a, b);
+      na = chain_step<OCT>(a, ra, ha.t, spa, sta);
+      nb = chain_step<OCT>(b, rb, hb.t, spb, stb);
+    }
+    chain_leaf(P, ra, ma, ha, na, spa, sta);
+    chain_leaf(P, rb, mb, hb, nb, spb, stb);
+    if (na == kChainDone || nb == kChainDone) break;
+  }
+  bool dummy = false;
+  if (na != kChainDone) traverse_fast_from<false, OCT>(P, ra, acta, ha, dummy, sta, na, spa);
+  else if (nb != kChainDone) traverse_fast_from<false, OCT>(P, rb, actb, hb, dummy, stb, nb, spb);
+  if (!acta) ha.t = INFINITY;
+  if (!actb) hb.t = INFINITY;
+}
+
+// both packets' closest hits: the dual loop when all their rays share one direction octant, else the
+// two single-chain walks one after the other (generic loop)
+__device__ __forceinline__ void trace_dual(const DevScene& P, const Ray& ra, const Ray& rb, bool acta, bool actb,
+                                           Hit& ha, Hit& hb, uint32_t* sta, uint32_t* stb) {
+  const uint64_t act = ballot(acta) | ballot(actb);
+  const uint64_t sx = (ballot(acta && (__float_as_uint(ra.id.x) >> 31)) | ballot(actb && (__float_as_uint(rb.id.x) >> 31))),
+                 sy = (ballot(acta && (__float_as_uint(ra.id.y) >> 31)) | ballot(actb && (__float_as_uint(rb.id.y) >> 31))),
+                 sz = (ballot(acta && (__float_as_uint(ra.id.z) >> 31)) | ballot(actb && (__float_as_uint(rb.id.z) >> 31)));
+  const uint64_t ax = ballot(acta && !(__float_as_uint(ra.id.x) >> 31)) | ballot(actb && !(__float_as_uint(rb.id.x) >> 31)),
+                 ay = ballot(acta && !(__float_as_uint(ra.id.y) >> 31)) | ballot(actb && !(__float_as_uint(rb.id.y) >> 31)),
+                 az = ballot(acta && !(__float_as_uint(ra.id.z) >> 31)) | ballot(actb && !(__float_as_uint(rb.id.z) >> 31));
+  if (act && (sx == 0 || ax == 0) && (sy == 0 || ay == 0) && (sz == 0 || az == 0)) {
+    const int oct = (sx ? 1 : 0) | (sy ? 2 : 0) | (sz ? 4 : 0);
+    switch (oct) {
+      case 0: traverse_dual<0>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      case 1: traverse_dual<1>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      case 2: traverse_dual<2>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      case 3: traverse_dual<3>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      case 4: traverse_dual<4>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      case 5: traverse_dual<5>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      case 6: traverse_dual<6>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+      default: traverse_dual<7>(P, ra, rb, acta, actb, ha, hb, sta, stb); return;
+    }
+  }
+  bool dummy = false;
+  traverse_fast<false, -1>(P, ra, acta, ha, dummy, sta);
+  traverse_fast<false, -1>(P, rb, actb, hb, dummy, stb);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1433,6 +1575,9 @@ __device__ __forceinline__ void traverse_x2(const DevScene& P, const Ray& ra, co
   }
 }
 
+#ifndef RT_DUAL_WAVES_PER_EU
+#define RT_DUAL_WAVES_PER_EU 8
+#endif
 #ifndef RT_X2_WAVES_PER_EU
 #define RT_X2_WAVES_PER_EU 6
 #endif
@@ -1560,6 +1705,51 @@ void k_primary_fused(FrameParams P) {
   trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
   if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
   wave_clock_end(P, lds.clk, c.lane, c.qw);
+}
+
+// PRIMARY with two 8x8 packets per wave (dual-chain traversal, traverse_dual): block b traces pair b
+// = the left and right 8x8 quarters of one 8-row half of a 16x16 tile; dispatch order as the one-wave
+// kernels (chunked XCD runs, or longest-first over pairs from an earlier frame's pair costs).
+struct PairCoord {
+  int lane, pair, pxa, py;
+  bool acta, actb;
+};
+__device__ __forceinline__ PairCoord pair_coord(const FrameParams& P) {
+  PairCoord c;
+  c.lane = threadIdx.x & 63;
+  int bid = (int)blockIdx.x;
+  if (RT_ORDER_LPT && P.order != nullptr) {
+    const uint32_t o = uniform(P.order[blockIdx.x]);
+    bid = o < gridDim.x ? (int)o : (int)blockIdx.x;
+  } else if (P.xcd_remap >= 2) {
+    const int C = P.xcd_remap, G = 8 * C, full = ((int)gridDim.x / G) * G;
+    if (bid < full) {
+      const int x = bid & 7, k = bid >> 3;
+      bid = (k / C) * G + x * C + (k % C);
+    }
+  }
+  c.pair = bid;
+  const int tile = P.shard_index + (bid >> 1) * P.shard_count;
+  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  c.pxa = tx * 16 + (c.lane & 7);
+  c.py = ty * 16 + (bid & 1) * 8 + (c.lane >> 3);
+  c.acta = c.pxa < P.W && c.py < P.H;
+  c.actb = c.pxa + 8 < P.W && c.py < P.H;
+  return c;
+}
+
+template <bool HITS, bool BOXCOL = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_DUAL_WAVES_PER_EU)))
+void k_primary_dual(FrameParams P) {
+  __shared__ WaveLds<TRAV_B2_LDS, false> lds;
+  wave_clock_start(P, lds.clk);
+  const PairCoord c = pair_coord(P);
+  const Ray ra = primary_ray(P, c.pxa, c.py), rb = primary_ray(P, c.pxa + 8, c.py);
+  Hit ha{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu}, hb{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  trace_dual(P.sc, ra, rb, c.acta, c.actb, ha, hb, lds.stack[0], lds.stack[1]);
+  if (c.acta) shade_primary_pixel<HITS, BOXCOL>(P, ra, (size_t)c.py * P.W + c.pxa, ha.t, ha.slot);
+  if (c.actb) shade_primary_pixel<HITS, BOXCOL>(P, rb, (size_t)c.py * P.W + c.pxa + 8, hb.t, hb.slot);
+  wave_clock_end(P, lds.clk, c.lane, c.pair);
 }
 
 // FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
@@ -2680,8 +2870,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   }
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
+  // PRIMARY with two packets per wave (k_primary_dual): variant bit 1048576
+  const bool dual = (fr->mode == RT_MODE_PRIMARY || fr->mode == RT_MODE_BOX_COLORS) && !stats &&
+                    (fr->max_depth <= 1 || fr->mode == RT_MODE_BOX_COLORS) && !(variant & (1 | 2 | 4 | 32768 | 256 | 2048 | 65536)) &&
+                    (variant & 1048576);
+  const size_t units = (size_t)grid * (dual ? 2 : 4);  // one-wave blocks of the render kernel
   if (fr->flags & RT_FRAME_TIMELINE) {  // one record per one-wave block of the render kernel
-    const size_t waves = (size_t)grid * 4;
+    const size_t waves = units;
     if (waves > slot.timeline_waves) {
       HIPCHECK(hipStreamSynchronize(st));
       if (slot.d_timeline) (void)hipFree(slot.d_timeline);
@@ -2729,7 +2924,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const bool lpt = one_wave_kernel && !(variant & 131072) && P.xcd_remap >= 2 && grid > 0 && (alone || (variant & 524288));
   bool lpt_sort = false;
   if (lpt) {
-    const size_t waves = (size_t)grid * 4;
+    const size_t waves = units;
     if (waves > slot.order_waves) {
       HIPCHECK(hipStreamSynchronize(st));
       if (slot.d_cost) (void)hipFree(slot.d_cost);
@@ -2779,7 +2974,18 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev_m, st));
   } else if (grid > 0) {
-    if (prim && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
+    if (dual && grid > 0) {
+      const dim3 g((unsigned)units), b(64);
+      if (boxcol) {
+        if (hits) hipLaunchKernelGGL((k_primary_dual<true, true>), g, b, 0, st, P);
+        else hipLaunchKernelGGL((k_primary_dual<false, true>), g, b, 0, st, P);
+      } else {
+        if (hits) hipLaunchKernelGGL((k_primary_dual<true, false>), g, b, 0, st, P);
+        else hipLaunchKernelGGL((k_primary_dual<false, false>), g, b, 0, st, P);
+      }
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipEventRecord(ev_m, st));
+    } else if (prim && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
       const dim3 g(grid * (4 / RT_TRACE_WPB)), b(64 * RT_TRACE_WPB);
       // RT_LDS_PAD (diagnostics): extra dynamic LDS per block, to cap the resident waves per CU in
       // occupancy experiments (160 KiB / (pad + 1 KiB) blocks per CU)
@@ -2834,7 +3040,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   }
   if (lpt_sort) {  // the next frame of this shape on this slot dispatches longest-first
     hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)slot.d_cost, slot.d_order,
-                       (int)(grid * 4), P.xcd_remap, (variant & 262144) ? 1 : 0);
+                       (int)units, P.xcd_remap, (variant & 262144) ? 1 : 0);
     HIPCHECK(hipGetLastError());
     slot.order_valid = true;
     slot.order_age = 0;
