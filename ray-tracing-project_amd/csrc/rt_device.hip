@@ -127,6 +127,19 @@ __device__ __forceinline__ Node64 sload_node_pf_carry(const Node64* base, uint32
   return r;
 }
 __device__ __forceinline__ TriRec64 sload_tri(const TriRec64* base, uint32_t i) { return sload64(base, i); }
+// node fetch by byte offset with one carried prefetch sink (RT_PF_MODE 1 / 2: the step's own s_waitcnt
+// retires the previous step's far-child prefetch)
+__device__ __forceinline__ Node64 sload_node_sink(const Node64* base, uint32_t h, uint32_t& sink) {
+  const uint32_t off = node_offset(__builtin_amdgcn_readfirstlane(h));
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  i16v v;
+  asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)" : "=&s"(v), "+&s"(sink) : "s"(bs), "s"(off) : "memory");
+  Node64 r;
+  __builtin_memcpy(&r, &v, 64);
+  return r;
+}
 
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -334,6 +347,9 @@ struct WaveStack {
 #ifndef RT_PREFETCH_PADLOAD  // 1: offsets re-loaded inside the node-load asm (0: tie-ordered separate asm, measured ±0.5%)
 #define RT_PREFETCH_PADLOAD 1
 #endif
+#ifndef RT_PF_MODE  // 0: both children prefetched at node arrival (RT_PREFETCH); 1: far child after the decision; 2: none
+#define RT_PF_MODE 0
+#endif
 #ifndef RT_PF_CARRY  // 1: prefetch sinks carried to the next node step (no wait at the end of a step)
 #define RT_PF_CARRY 1
 #endif
@@ -491,11 +507,16 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
 #if RT_PREFETCH && RT_PF_CARRY
   uint32_t cpf0 = 0, cpf1 = 0;  // prefetch sinks, live across the traversal
 #endif
+  uint32_t fsink = 0;  // RT_PF_MODE 1: the far-child prefetch's sink
   uint32_t tos = 0;  // RT_TOS: lds_stack[sp - 1] while sp > 0
   for (;;) {
     while (!is_leaf(node)) {
       const int sp_before = sp;
-#if RT_PREFETCH && RT_PF_CARRY
+      const uint32_t cur_off = node_offset(uniform(node));  // RT_PF_MODE 1
+#if RT_PF_MODE != 0
+      // 1: the far child is prefetched after the decision, only when it is pushed; 2: no prefetch
+      const Node64 nd = sload_node_sink(P.nodes, node, fsink);
+#elif RT_PREFETCH && RT_PF_CARRY
       const Node64 nd = sload_node_pf_carry(P.nodes, node, cpf0, cpf1);
 #elif RT_PREFETCH
       uint32_t pf0, pf1;
@@ -528,6 +549,15 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
               [c1] "s"(uniform(nd.child1))
             : "scc");
         lds_push(lds_stack + sp, farb);
+      }
+      uint32_t pf_far = 0;
+      if (RT_PF_MODE == 1 && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
+        asm("s_bitcmp1_b32 %[bits], %[oct]\n\t"
+            "s_cselect_b32 %[pf], %[p0], %[p1]"
+            : [pf] "=&s"(pf_far)
+            : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [p0] "s"(uniform(nd.pad0)),
+              [p1] "s"(uniform(nd.pad1))
+            : "scc");
       }
       const float tcut = ANY ? tlim : h.t;
       const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
@@ -566,6 +596,19 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
         far = farb;
         (void)ta;
         (void)tb;
+        if (RT_PF_MODE == 1) {
+          // the pushed far child's record into the scalar cache for its pop (the current node's own line,
+          // a hit, when nothing was pushed)
+          const uint64_t bb = (uint64_t)P.nodes;
+          const uint64_t bs = ((uint64_t)uniform((uint32_t)(bb >> 32)) << 32) | (uint32_t)uniform((uint32_t)bb);
+          uint32_t a;
+          asm volatile("s_cmp_lg_u32 %[sp], %[sp0]\n\t"
+                       "s_cselect_b32 %[a], %[pf], %[cur]\n\t"
+                       "s_load_dword %[sink], %[base], %[a]"
+                       : [sink] "+&s"(fsink), [a] "=&s"(a)
+                       : [sp] "s"(sp), [sp0] "s"((uint32_t)sp_before), [pf] "s"(pf_far), [cur] "s"(cur_off), [base] "s"(bs)
+                       : "scc", "memory");
+        }
       } else if (RT_ORDER_BITS && OCT >= 0) {
         // near child from the node's order bit for this octant (Node64::pad0), overridden when only
         // one child is needed
@@ -677,6 +720,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
 #if RT_PREFETCH && RT_PF_CARRY
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(cpf0), "s"(cpf1) : "memory");  // the last prefetches landed
 #endif
+  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(fsink) : "memory");
   if (!ANY && !active) h.t = INFINITY;
 }
 
