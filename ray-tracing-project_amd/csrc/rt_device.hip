@@ -347,7 +347,8 @@ struct WaveStack {
 #ifndef RT_PREFETCH_PADLOAD  // 1: offsets re-loaded inside the node-load asm (0: tie-ordered separate asm, measured ±0.5%)
 #define RT_PREFETCH_PADLOAD 1
 #endif
-#ifndef RT_PF_MODE  // 0: both children prefetched at node arrival (RT_PREFETCH); 1: far child after the decision; 2: none
+#ifndef RT_PF_MODE  // 0: both children prefetched at node arrival (RT_PREFETCH); 1: far child after the decision; 2: none;
+                    // 3: the near child (octant order bit) at node arrival
 #define RT_PF_MODE 0
 #endif
 #ifndef RT_PF_CARRY  // 1: prefetch sinks carried to the next node step (no wait at the end of a step)
@@ -549,6 +550,20 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
               [c1] "s"(uniform(nd.child1))
             : "scc");
         lds_push(lds_stack + sp, farb);
+      }
+      if (RT_PF_MODE == 3 && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
+        // the near child (the next node whenever it is needed) into the scalar cache, now: the next
+        // step's wait then covers this one line, not the far child's too
+        const uint64_t bb = (uint64_t)P.nodes;
+        const uint64_t bs = ((uint64_t)uniform((uint32_t)(bb >> 32)) << 32) | (uint32_t)uniform((uint32_t)bb);
+        uint32_t a;
+        asm volatile("s_bitcmp1_b32 %[bits], %[oct]\n\t"
+                     "s_cselect_b32 %[a], %[p1], %[p0]\n\t"
+                     "s_load_dword %[sink], %[base], %[a]"
+                     : [sink] "+&s"(fsink), [a] "=&s"(a)
+                     : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [p0] "s"(uniform(nd.pad0)),
+                       [p1] "s"(uniform(nd.pad1)), [base] "s"(bs)
+                     : "scc", "memory");
       }
       uint32_t pf_far = 0;
       if (RT_PF_MODE == 1 && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
