@@ -1945,13 +1945,14 @@ __device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r
 
 // Occupancy of the FULL megakernel, by scene: 8 waves per SIMD (64 VGPR + a 144-B spill) for scenes
 // whose node + triangle records exceed the chip's aggregate L2 (the 1M soup: 8 waves beat 5 by 18% and
-// 3 by 24% -- the traversal waits on L2 misses and needs the waves), a 5-wave bound (79 VGPR, no
-// spill, so 6 waves) for smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident).
+// 3 by 24% -- the traversal waits on L2 misses and needs the waves), a 6-wave bound (79 VGPR, no
+// spill) for smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident; the 5-wave bound
+// let the kernel grow to 82 VGPR = 5 waves, 4.6% slower; 7 waves spill 48 B, equal to 6).
 #ifndef RT_FULL_WAVES_PER_EU
 #define RT_FULL_WAVES_PER_EU 8
 #endif
 #ifndef RT_FULL_WAVES_PER_EU_SMALL
-#define RT_FULL_WAVES_PER_EU_SMALL 5
+#define RT_FULL_WAVES_PER_EU_SMALL 6
 #endif
 constexpr size_t kFullSmallSceneBytes = 32u << 20;  // 8 XCDs x 4 MiB L2
 #ifndef RT_FULL_WPB
@@ -2726,7 +2727,7 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 // reflection hits / the shadow rays of primary hits; 256 = two rays per lane (PRIMARY), 2048 =
 // persistent-threads PRIMARY traversal with per-XCD work counters (4096: without stealing); 32768 =
 // PRIMARY as trace + shade kernels instead of the fused k_primary_fused; 8192 /
-// 16384 = the FULL megakernel's 8-wave / small-scene (5-wave) build regardless of the scene size;
+// 16384 = the FULL megakernel's 8-wave / small-scene (6-wave) build regardless of the scene size;
 // 65536 = the generic traceRay kernel (k_render_depth) also at the modes' own depths; 131072 = the
 // default chunked-XCD dispatch order instead of longest-first (k_order_lpt); 262144 = longest-first
 // with half as many cost buckets (2 per octave: coarser, more spatial order kept); 524288 = longest-first

@@ -205,7 +205,7 @@ def test_stats_counting_run(rt, soup):
 
 VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-pipeline": 16, "pipeline-lane-refl": 48,
             "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
-            "persistent-no-steal": 2048 | 4096, "full-8-waves": 8192, "full-5-waves": 16384,
+            "persistent-no-steal": 2048 | 4096, "full-8-waves": 8192, "full-small-build": 16384,
             "split-primary": 32768, "generic-depth-kernel": 65536, "dual-chain": 1048576}
 
 
