@@ -994,7 +994,54 @@ uint32_t octant_order(const Node64& nd) {
 
 // interior nodes re-laid out depth-first (near child first) from `root`; unreferenced nodes dropped;
 // sets hs.nodes, hs.root = 0, hs.depth (levels of interior nodes + the leaf level)
+// Sibling-pair layout (RT_NODE_LAYOUT=pairs, A/B): the two interior children of a node occupy one
+// 128-B aligned pair of records (one L2 line on MI355X), depth first over the pairs; a node with one
+// interior child leaves the second record of its pair empty (never referenced). Root at 0, record 1 empty.
+static void relayout_pairs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) {
+  Node64 empty;
+  memset(&empty, 0, sizeof empty);
+  empty.c0lx = empty.c0ly = empty.c0lz = empty.c1lx = empty.c1ly = empty.c1lz = INFINITY;
+  empty.c0hx = empty.c0hy = empty.c0hz = empty.c1hx = empty.c1hy = empty.c1hz = -INFINITY;
+  empty.child0 = empty.child1 = make_leaf(0, 1);
+  std::vector<uint32_t> remap(tmp.size(), UINT32_MAX);
+  std::vector<uint32_t> slot_src{root, UINT32_MAX};  // record index -> source node (UINT32_MAX = empty)
+  remap[root] = 0;
+  std::vector<std::pair<uint32_t, int>> st{{root, 1}};
+  int depth = 0;
+  while (!st.empty()) {
+    const auto [n, d] = st.back();
+    st.pop_back();
+    depth = std::max(depth, d + 1);
+    const Node64& nd = tmp[n];
+    const bool i0 = !is_leaf(nd.child0), i1 = !is_leaf(nd.child1);
+    if (!i0 && !i1) continue;
+    const uint32_t base = (uint32_t)slot_src.size();
+    slot_src.push_back(UINT32_MAX);
+    slot_src.push_back(UINT32_MAX);
+    uint32_t k = base;
+    if (i0) { remap[nd.child0] = k; slot_src[k++] = nd.child0; }
+    if (i1) { remap[nd.child1] = k; slot_src[k++] = nd.child1; }
+    if (i1) st.push_back({nd.child1, d + 1});
+    if (i0) st.push_back({nd.child0, d + 1});
+  }
+  hs.nodes.resize(slot_src.size());
+  hs.leaves = 0;
+  for (size_t i = 0; i < slot_src.size(); i++) {
+    if (slot_src[i] == UINT32_MAX) { hs.nodes[i] = empty; continue; }
+    Node64 nd = tmp[slot_src[i]];
+    if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
+    if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
+    hs.leaves += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
+    nd.pad0 = octant_order(nd);
+    hs.nodes[i] = nd;
+  }
+  hs.root = 0;
+  hs.depth = depth;
+}
+
 void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) {
+  static const bool pairs = [] { const char* e = getenv("RT_NODE_LAYOUT"); return e && !strcmp(e, "pairs"); }();
+  if (pairs) { relayout_pairs(hs, tmp, root); return; }
   std::vector<uint32_t> remap(tmp.size(), UINT32_MAX), order;
   std::vector<std::pair<uint32_t, int>> st{{root, 1}};
   int depth = 0;
