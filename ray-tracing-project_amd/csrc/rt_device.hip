@@ -348,7 +348,8 @@ struct WaveStack {
 #define RT_PREFETCH_PADLOAD 1
 #endif
 #ifndef RT_PF_MODE  // 0: both children prefetched at node arrival (RT_PREFETCH); 1: far child after the decision; 2: none;
-                    // 3: the near child (octant order bit) at node arrival
+                    // 3: the near child (octant order bit) at node arrival; 4: 3 + the far child's line
+                    // into L2 by a vector load; 5: both children by vector loads
 #define RT_PF_MODE 0
 #endif
 #ifndef RT_PF_CARRY  // 1: prefetch sinks carried to the next node step (no wait at the end of a step)
@@ -508,7 +509,8 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
 #if RT_PREFETCH && RT_PF_CARRY
   uint32_t cpf0 = 0, cpf1 = 0;  // prefetch sinks, live across the traversal
 #endif
-  uint32_t fsink = 0;  // RT_PF_MODE 1: the far-child prefetch's sink
+  uint32_t fsink = 0;  // RT_PF_MODE 1 / 3 / 4: the scalar prefetch's sink
+  uint32_t vsink0 = 0, vsink1 = 0;  // RT_PF_MODE 4 / 5: the vector prefetches' sinks
   uint32_t tos = 0;  // RT_TOS: lds_stack[sp - 1] while sp > 0
   for (;;) {
     while (!is_leaf(node)) {
@@ -550,6 +552,25 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
               [c1] "s"(uniform(nd.child1))
             : "scc");
         lds_push(lds_stack + sp, farb);
+      }
+      if ((RT_PF_MODE == 4 || RT_PF_MODE == 5) && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
+        // 4: the far child's line into L2 by one vector load (its own counter: no scalar wait is tied to
+        // it; the pop reads it from L2), the near child by a scalar prefetch as in 3; 5: both by vector loads
+        const uint32_t o0 = uniform(nd.pad0), o1 = uniform(nd.pad1);
+        uint32_t fa, na;
+        asm("s_bitcmp1_b32 %[bits], %[oct]\n\t"
+            "s_cselect_b32 %[fa], %[p0], %[p1]\n\t"
+            "s_cselect_b32 %[na], %[p1], %[p0]"
+            : [fa] "=&s"(fa), [na] "=&s"(na)
+            : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [p0] "s"(o0), [p1] "s"(o1)
+            : "scc");
+        const uint64_t bb = (uint64_t)P.nodes;
+        const uint64_t bs = ((uint64_t)uniform((uint32_t)(bb >> 32)) << 32) | (uint32_t)uniform((uint32_t)bb);
+        asm volatile("global_load_dword %0, %1, %2" : "+&v"(vsink0) : "v"(fa & ~3u), "s"(bs) : "memory");
+        if (RT_PF_MODE == 5)
+          asm volatile("global_load_dword %0, %1, %2" : "+&v"(vsink1) : "v"(na & ~3u), "s"(bs) : "memory");
+        else
+          asm volatile("s_load_dword %0, %1, %2" : "+&s"(fsink) : "s"(bs), "s"(na) : "memory");
       }
       if (RT_PF_MODE == 3 && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
         // the near child (the next node whenever it is needed) into the scalar cache, now: the next
@@ -736,6 +757,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(cpf0), "s"(cpf1) : "memory");  // the last prefetches landed
 #endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(fsink) : "memory");
+  if (RT_PF_MODE == 4 || RT_PF_MODE == 5) asm volatile("s_waitcnt vmcnt(0)" ::"v"(vsink0), "v"(vsink1) : "memory");
   if (!ANY && !active) h.t = INFINITY;
 }
 
