@@ -57,10 +57,23 @@ def frame_for(n_gpus, override):
     return (1920, 1080) if n_gpus == 1 else (3840, 2160)
 
 
+SHARD_SUPER_TILE = 4  # rt_internal.h kShardSuperTile
+
+
 def shard_tiles(W, H, rank, n):
-    """16x16 tiles this rank renders (the kernel's assignment: tile t goes to rank t % n)."""
-    tx = (W + 15) // 16
-    return [(t % tx, t // tx) for t in range(rank, tx * ((H + 15) // 16), n)]
+    """16x16 tiles this rank renders, in its slot order (rt_api.h rt_frame.shard_index: with n > 1 the
+    tiles are grouped into 4x4 super-tiles, super-tile s going to rank s % n; rt_frame_shard_tiles)."""
+    tx, ty = (W + 15) // 16, (H + 15) // 16
+    S = SHARD_SUPER_TILE if n > 1 else 1
+    sxn = (tx + S - 1) // S
+    ns = sxn * ((ty + S - 1) // S)
+    out = []
+    for s in range(rank, ns, n):
+        for k in range(S * S):
+            x, y = (s % sxn) * S + k % S, (s // sxn) * S + k // S
+            if x < tx and y < ty:
+                out.append((x, y))
+    return out
 
 
 def cpu_threads():
@@ -229,7 +242,14 @@ def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_de
     st = sc.synchronize()
     sync_device()
     barrier()
-    return time.perf_counter() - t0, st
+    el = time.perf_counter() - t0
+    # host cost of queueing one frame (rt_render_async through the Python binding), frames not waited on
+    t1 = time.perf_counter()
+    for _ in range(min(steps, 3)):
+        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    st["enqueue_ms"] = (time.perf_counter() - t1) / min(steps, 3) * 1e3
+    sc.synchronize()
+    return el, st
 
 
 def isolated_kernel_ms(rt, sc, cam, W, H, mode, shard, iters=20):
@@ -263,6 +283,9 @@ def main():
                     help="BVH builder: host binned SAH (default) or the device LBVH (SURVEY f2)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames that may overlap on the GPU (0 = library default, 4)")
+    ap.add_argument("--rehearse-shards", type=int, default=0,
+                    help="one GPU renders only shard 0 of K (the per-GPU work of a K-GPU C4 run, no collective): "
+                         "rehearsal of strong scaling; the line reports that shard's rate")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -300,7 +323,10 @@ def main():
 
     rt = load_rtamd()
     ident = rt.build_identity()
-    W, H = frame_for(n, a.frame)
+    K = a.rehearse_shards if (a.rehearse_shards > 1 and n == 1) else 0
+    if K:
+        a.no_cpu = True
+    W, H = frame_for(K or n, a.frame)
     t0 = time.perf_counter()
     if a.scene == "soup":
         mesh, _, _ = rt.soup_mesh(a.tris, 12345)
@@ -315,7 +341,7 @@ def main():
     setup_s = time.perf_counter() - t0
     cam = rt.flycam(W, H, 0, 0, 20)
     mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY
-    shard = (rank, n)
+    shard = (0, K) if K else (rank, n)
 
     elapsed, st = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device)
     my_rays = st["primary_rays"] * a.steps
@@ -332,7 +358,7 @@ def main():
     # the second frame size: N = 1 -> the C4 frame on this one GPU (strong-scaling base of C4);
     # N > 1 -> the metric's 1080p frame split over the N ranks
     extra = None
-    if not a.no_extra and a.frame is None and a.scene == "soup":
+    if not a.no_extra and a.frame is None and a.scene == "soup" and not K:
         W2, H2 = (3840, 2160) if n == 1 else (1920, 1080)
         cam2 = rt.flycam(W2, H2, 0, 0, 20)
         k2 = max(10, a.steps // 2)
@@ -423,7 +449,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": f"{cname}: {scene_name}, {W}x{H} {a.mode} rays, eye (0,0,1), 1 light"
-                                   + (f", split over {n} GPUs" if n > 1 else ""),
+                                   + (f", split over {n} GPUs" if n > 1 else "")
+                                   + (f", REHEARSAL: shard 0 of {K} on one GPU (value = that shard's rate)" if K else ""),
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
                        "parallelism": f"tiles/{n} (16x16 tiles interleaved over ranks, scene replicated)",
                        "frames_in_flight": info_fif,
@@ -431,6 +458,7 @@ def main():
                        # frame; frames overlap, so ms_per_step is the throughput interval) and alone
                        "kernel_ms_per_frame": round(kernel_ms_max, 4),
                        "kernel_ms_one_frame_alone": round(iso_ms_max, 4),
+                       "host_enqueue_ms_per_frame": round(st.get("enqueue_ms", 0.0), 4),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
                        "builder": "lbvh-gpu" if info["builder"] == 1 else "sah-host",

@@ -212,8 +212,11 @@ typedef struct rt_frame {
                           (flyscene.hpp:166, flyscene.cpp:334-348): a hit pixel is the sum of the colours
                           of every reference box that hasFace() the closest face, unclamped, no shading,
                           shadows or reflection (a miss: the background); colours: rt_scene_set_box_colors */
-  int32_t shard_index; /* this device renders the 16x16 tiles t (row-major over the frame) with
-                          t % shard_count == shard_index */
+  int32_t shard_index; /* this device renders its share of the frame's 16x16-pixel tiles: with
+                          shard_count > 1 the tiles are grouped into 4x4-tile super-tiles (64x64 pixels;
+                          row-major over the frame, partial at the right / bottom edges) and super-tile s
+                          belongs to shard s % shard_count (an XCD's concurrent waves then trace
+                          neighbouring pixels); rt_frame_shard_tiles lists them */
   int32_t shard_count; /* 1 = whole frame */
   int32_t flags;       /* RT_FRAME_* */
   int32_t max_depth;   /* traceRay's recursion limit (Flyscene::max_depth, flyscene.hpp:142; the reference
@@ -276,6 +279,10 @@ int rt_frame_download_rgb8(rt_scene* s, int64_t capacity_pixels, uint8_t* rgb8, 
  * after their device work is complete, and the caller orders any earlier writes to those buffers made on
  * other streams (the library's streams do not synchronise with the legacy default stream). */
 int64_t rt_frame_shard_bytes(int32_t width, int32_t height, int32_t shard_count);
+/* The 16x16 tiles shard shard_index of shard_count renders, in its slot order (the order of its packed
+ * slice; slots of super-tile tiles outside the frame are skipped here and zero in the slice): tiles_xy
+ * [n][2] = (tile x, tile y), NULL = count only. Returns n. */
+int32_t rt_frame_shard_tiles(int32_t width, int32_t height, int32_t shard_index, int32_t shard_count, int32_t* tiles_xy);
 int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device);
 int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t shard_count, int32_t width, int32_t height,
                                 void* frame_device, int32_t device);

@@ -1403,8 +1403,8 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
     const int q = nb >> 3, rr = nb & 7, x = b & 7, k = b >> 3;
     L = x < rr ? x * (q + 1) + k : rr * (q + 1) + (x - rr) * q + k;
   }
-  const int tile = P.shard_index + L * P.shard_count;
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  int tx, ty;
+  shard_tile_xy(P.tiles_x, P.super_tile, P.shard_index, P.shard_count, L, tx, ty);
   c.px = tx * 16 + (c.wv & 1) * 8 + (c.lane & 7);
   c.py = ty * 16 + (c.wv >> 1) * 8 + (c.lane >> 3);
   c.active = c.px < P.W && c.py < P.H;
@@ -1600,8 +1600,8 @@ void k_trace_primary_persistent(FrameParams P, uint32_t* queue, uint32_t max_ste
     const uint32_t xk = (x0 + k) & 7u;
     const uint32_t nxt_i = take(xk);  // the next item from the same counter, requested early
     const int b = (int)(cur >> 2), wv = (int)(cur & 3);
-    const int tile = P.shard_index + b * P.shard_count;
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    int tx, ty;
+    shard_tile_xy(P.tiles_x, P.super_tile, P.shard_index, P.shard_count, b, tx, ty);
     const int px = tx * 16 + (wv & 1) * 8 + (lane & 7), py = ty * 16 + (wv >> 1) * 8 + (lane >> 3);
     const bool active = px < P.W && py < P.H;
     const Ray r = primary_ray(P, px, py);
@@ -1670,8 +1670,8 @@ void k_trace_primary_x2(FrameParams P) {
   const int lane = threadIdx.x & 63;
   const int nb = (int)(gridDim.x >> 1), b = (int)(blockIdx.x >> 1), half = (int)(blockIdx.x & 1);
   (void)nb;
-  const int tile = P.shard_index + b * P.shard_count;
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  int tx, ty;
+  shard_tile_xy(P.tiles_x, P.super_tile, P.shard_index, P.shard_count, b, tx, ty);
   const int pxa = tx * 16 + (lane & 7), pxb = pxa + 8, py = ty * 16 + half * 8 + (lane >> 3);
   const bool acta = pxa < P.W && py < P.H, actb = pxb < P.W && py < P.H;
   const Ray ra = primary_ray(P, pxa, py), rb = primary_ray(P, pxb, py);
@@ -1810,8 +1810,8 @@ __device__ __forceinline__ PairCoord pair_coord(const FrameParams& P) {
     }
   }
   c.pair = bid;
-  const int tile = P.shard_index + (bid >> 1) * P.shard_count;
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  int tx, ty;
+  shard_tile_xy(P.tiles_x, P.super_tile, P.shard_index, P.shard_count, bid >> 1, tx, ty);
   c.pxa = tx * 16 + (c.lane & 7);
   c.py = ty * 16 + (bid & 1) * 8 + (c.lane >> 3);
   c.acta = c.pxa < P.W && c.py < P.H;
@@ -2468,11 +2468,12 @@ __device__ __forceinline__ uint8_t ppm_u8(float c) {
   return (uint8_t)max(min(255, v), 0);
 }
 __global__ __launch_bounds__(256) void k_pack_shard(const float* rgb, uint8_t* out, int W, int H, int tiles_x,
-                                                    int si, int sc, int n_tiles) {
-  const int L = blockIdx.x;  // one block per tile of the shard, one thread per pixel
+                                                    int si, int sc, int n_tiles, int S) {
+  const int L = blockIdx.x;  // one block per tile slot of the shard, one thread per pixel
   if (L >= n_tiles) return;
-  const int tile = si + L * sc;
-  const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
+  int tx, ty;
+  shard_tile_xy(tiles_x, S, si, sc, L, tx, ty);
+  const int x = tx * 16 + (threadIdx.x & 15), y = ty * 16 + (threadIdx.x >> 4);
   uint8_t* o = out + ((size_t)L * 256 + threadIdx.x) * 3;
   if (x < W && y < H) {
     const float* c = rgb + 3 * ((size_t)y * W + x);
@@ -2484,12 +2485,14 @@ __global__ __launch_bounds__(256) void k_pack_shard(const float* rgb, uint8_t* o
   }
 }
 __global__ __launch_bounds__(256) void k_unpack_shards(const uint8_t* packed, uint8_t* frame, int W, int H, int tiles_x,
-                                                       int n, size_t slice_bytes) {
+                                                       int n, size_t slice_bytes, int S) {
   const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= (size_t)W * H) return;
   const int x = (int)(p % W), y = (int)(p / W);
-  const int t = (y >> 4) * tiles_x + (x >> 4);
-  const uint8_t* src = packed + (size_t)(t % n) * slice_bytes + ((size_t)(t / n) * 256 + (y & 15) * 16 + (x & 15)) * 3;
+  // the inverse of shard_tile_xy: tile -> super-tile s -> (owner s % n, slot (s / n) * S^2 + in-super index)
+  const int tx = x >> 4, ty = y >> 4, sxn = (tiles_x + S - 1) / S;
+  const int s = (ty / S) * sxn + tx / S, slot = (s / n) * S * S + (ty % S) * S + tx % S;
+  const uint8_t* src = packed + (size_t)(s % n) * slice_bytes + ((size_t)slot * 256 + (y & 15) * 16 + (x & 15)) * 3;
   frame[3 * p + 0] = src[0];
   frame[3 * p + 1] = src[1];
   frame[3 * p + 2] = src[2];
@@ -2866,6 +2869,19 @@ extern "C" int rt_device_count(void) {
   return n;
 }
 
+// Super-tile width of a shard_count-way split (shard_tile_xy, rt_api.h rt_frame): 4x4 tiles (64x64
+// pixels) per super-tile when the frame is split, so that the waves an XCD runs together trace
+// neighbouring pixels (the rank's L2 working set stays compact): C4 over 8 / 4 GPUs +10% / +7% per GPU
+// against single tiles interleaved (profiles/ab/r02_super_tiles_ab.txt); an unsplit frame keeps its tile
+// order (super-tiles there: C3 ±1%, C4 -3%). RT_SUPER_TILE (A/B) overrides it inside the library; the
+// shard-tile helpers (rt_frame_shard_tiles, pack / unpack, rt_frame_shard_bytes) follow the same rule.
+static int frame_super_tile(int shard_count) {
+  static const int env = [] { const char* e = getenv("RT_SUPER_TILE"); return e ? atoi(e) : 0; }();
+  if (kernel_variant() & 16) return 1;  // the FULL stage pipeline sizes its lists by the frame's own tiles
+  if (env > 0) return env;
+  return shard_count > 1 ? kShardSuperTile : 1;
+}
+
 extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
                                const rt_frame* fr) {
   int rc = check_device_scene(s);
@@ -2932,7 +2948,9 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   const int ntiles = P.tiles_x * P.tiles_y;
   P.shard_index = si;
   P.shard_count = sc;
-  P.n_tiles_shard = ntiles > si ? (ntiles - si + sc - 1) / sc : 0;
+  P.super_tile = frame_super_tile(sc);
+  P.n_tiles_shard = shard_tile_slots(P.tiles_x, P.tiles_y, P.super_tile, si, sc);
+  (void)ntiles;
   P.mode = fr->mode;
   P.flags = fr->flags;
   P.rgb = slot.d_rgb;
@@ -3138,9 +3156,11 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   s->last_flags = fr->flags;
   // primary rays of this shard: pixels inside the frame of the shard's tiles
   int64_t rays = 0;
-  for (int t = si; t < ntiles; t += sc) {
-    const int tx = t % P.tiles_x, ty = t / P.tiles_x;
-    rays += (int64_t)std::min(16, fr->width - tx * 16) * std::min(16, fr->height - ty * 16);
+  for (int L = 0; L < P.n_tiles_shard; L++) {
+    int tx, ty;
+    shard_tile_xy(P.tiles_x, P.super_tile, si, sc, L, tx, ty);
+    if (tx < P.tiles_x && ty < P.tiles_y)
+      rays += (int64_t)std::min(16, fr->width - tx * 16) * std::min(16, fr->height - ty * 16);
   }
   s->last_rays = rays;
   s->pending = true;
@@ -3243,8 +3263,23 @@ extern "C" int rt_frame_download_rgb8(rt_scene* s, int64_t capacity_pixels, uint
 
 extern "C" int64_t rt_frame_shard_bytes(int32_t W, int32_t H, int32_t shard_count) {
   if (W <= 0 || H <= 0 || shard_count <= 0) return 0;
-  const int64_t ntiles = (int64_t)((W + 15) / 16) * ((H + 15) / 16);
-  return (ntiles + shard_count - 1) / shard_count * 768;
+  // shard 0 has the most tile slots
+  return (int64_t)shard_tile_slots((W + 15) / 16, (H + 15) / 16, frame_super_tile(shard_count), 0, shard_count) * 768;
+}
+
+extern "C" int32_t rt_frame_shard_tiles(int32_t W, int32_t H, int32_t shard_index, int32_t shard_count, int32_t* tiles_xy) {
+  if (W <= 0 || H <= 0 || shard_count <= 0 || shard_index < 0 || shard_index >= shard_count) return 0;
+  const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16, S = frame_super_tile(shard_count);
+  const int slots = shard_tile_slots(tiles_x, tiles_y, S, shard_index, shard_count);
+  int32_t n = 0;
+  for (int L = 0; L < slots; L++) {
+    int tx, ty;
+    shard_tile_xy(tiles_x, S, shard_index, shard_count, L, tx, ty);
+    if (tx >= tiles_x || ty >= tiles_y) continue;
+    if (tiles_xy) { tiles_xy[2 * n] = tx; tiles_xy[2 * n + 1] = ty; }
+    n++;
+  }
+  return n;
 }
 
 extern "C" int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device) {
@@ -3253,15 +3288,15 @@ extern "C" int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device) {
   if (!dst_device) { set_error("rt_frame_pack_shard_rgb8: null destination"); return RT_ERR_INVALID; }
   rt_scene::FrameSlot& f = s->slots[s->last_slot];
   if (!f.d_rgb || (size_t)s->last_W * s->last_H > f.fb_pixels) { set_error("rt_frame_pack_shard_rgb8: no frame rendered"); return RT_ERR_INVALID; }
-  const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, ntiles = tiles_x * ((H + 15) / 16);
-  const int si = s->last_shard_index, sc = s->last_shard_count;
-  const int n_tiles = ntiles > si ? (ntiles - si + sc - 1) / sc : 0;
+  const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
+  const int si = s->last_shard_index, sc = s->last_shard_count, S = frame_super_tile(sc);
+  const int n_tiles = shard_tile_slots(tiles_x, tiles_y, S, si, sc);
   hipStream_t st = (hipStream_t)f.stream;
   const int64_t slice = rt_frame_shard_bytes(W, H, sc);
   if ((int64_t)n_tiles * 768 < slice) HIPCHECK(hipMemsetAsync((uint8_t*)dst_device + (size_t)n_tiles * 768, 0, (size_t)(slice - (int64_t)n_tiles * 768), st));
   if (n_tiles > 0)
     hipLaunchKernelGGL(k_pack_shard, dim3(n_tiles), dim3(256), 0, st, (const float*)f.d_rgb, (uint8_t*)dst_device, W, H,
-                       tiles_x, si, sc, n_tiles);
+                       tiles_x, si, sc, n_tiles, S);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(st));
   return RT_OK;
@@ -3278,7 +3313,8 @@ extern "C" int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t sh
   HIPCHECK(hipSetDevice(dev));
   const size_t npix = (size_t)W * H;
   hipLaunchKernelGGL(k_unpack_shards, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, 0, (const uint8_t*)packed_device,
-                     (uint8_t*)frame_device, W, H, (W + 15) / 16, shard_count, (size_t)rt_frame_shard_bytes(W, H, shard_count));
+                     (uint8_t*)frame_device, W, H, (W + 15) / 16, shard_count, (size_t)rt_frame_shard_bytes(W, H, shard_count),
+                     frame_super_tile(shard_count));
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipDeviceSynchronize());
   return RT_OK;
@@ -3295,9 +3331,12 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* ligh
   if (sc == 1) return rt_frame_download(s, (int64_t)W * H, out_rgb, nullptr, nullptr);
   std::vector<float> full((size_t)W * H * 3);
   if ((rc = rt_frame_download(s, (int64_t)W * H, full.data(), nullptr, nullptr))) return rc;
-  const int tiles_x = (W + 15) / 16, ntiles = tiles_x * ((H + 15) / 16);
-  for (int t = fr->shard_index; t < ntiles; t += sc) {
-    const int tx = t % tiles_x, ty = t / tiles_x;
+  const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16, S = frame_super_tile(sc);
+  const int slots = shard_tile_slots(tiles_x, tiles_y, S, fr->shard_index, sc);
+  for (int L = 0; L < slots; L++) {
+    int tx, ty;
+    shard_tile_xy(tiles_x, S, fr->shard_index, sc, L, tx, ty);
+    if (tx >= tiles_x || ty >= tiles_y) continue;
     for (int y = ty * 16; y < std::min(H, ty * 16 + 16); y++) {
       const size_t o = ((size_t)y * W + tx * 16) * 3;
       memcpy(out_rgb + o, full.data() + o, sizeof(float) * 3 * (size_t)(std::min(W, tx * 16 + 16) - tx * 16));

@@ -42,6 +42,30 @@ RT_HD uint32_t make_leaf(uint32_t first, uint32_t count) {
   return kLeafBit | ((count - 1u) << kLeafCountShift) | first;
 }
 
+// Shard tiling (rt_frame.shard_index / shard_count): the frame is cut into 16x16-pixel tiles, grouped
+// into S x S super-tiles (S = super); super-tile s (row-major over the frame) belongs to shard s % count,
+// and shard i's L-th tile is tile k = L % S^2 (row-major) of its (L / S^2)-th super-tile. S = 1: tile t
+// goes to shard t % count. Tiles of a super-tile that fall outside the frame are still enumerated (their
+// pixels are inactive), so every shard has ceil(n_super / count) * S^2 slots.
+constexpr int kShardSuperTile = 4;  // super-tile width (tiles) of a split frame
+RT_HD int shard_super_count(int tiles_x, int tiles_y, int S) { return ((tiles_x + S - 1) / S) * ((tiles_y + S - 1) / S); }
+RT_HD int shard_tile_slots(int tiles_x, int tiles_y, int S, int index, int count) {
+  const int ns = shard_super_count(tiles_x, tiles_y, S);
+  return ns > index ? (ns - index + count - 1) / count * S * S : 0;
+}
+RT_HD void shard_tile_xy(int tiles_x, int S, int index, int count, int L, int& tx, int& ty) {
+  if (S <= 1) {
+    const int t = index + L * count;
+    tx = t % tiles_x;
+    ty = t / tiles_x;
+    return;
+  }
+  const int S2 = S * S, j = L / S2, k = L - j * S2;
+  const int s = index + j * count, sx_n = (tiles_x + S - 1) / S;
+  tx = (s % sx_n) * S + k % S;
+  ty = (s / sx_n) * S + k / S;
+}
+
 struct alignas(16) Node64 {
   // child 0: lo.x hi.x lo.y hi.y | lo.z hi.z ; child 1: lo.x hi.x | lo.y hi.y lo.z hi.z
   float c0lx, c0hx, c0ly, c0hy;
@@ -135,6 +159,7 @@ struct FrameParams {
   int32_t W, H, tiles_x, tiles_y;  // tiles = 16x16 pixel blocks (one 256-thread block each)
   int32_t xcd_remap;
   int32_t shard_index, shard_count, n_tiles_shard;
+  int32_t super_tile;         // S of shard_tile_xy (1: tile t -> shard t % count)
   int32_t mode, flags;
   int32_t max_depth;          // k_render_depth: traceRay's recursion limit (flyscene.hpp:142)
   int32_t shadows;            // k_render_depth: shadow() per light (FULL) or not (PRIMARY)

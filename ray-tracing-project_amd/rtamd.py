@@ -31,7 +31,7 @@ EXPORTS = [
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
-    "rt_debug_timeline", "rt_box_colors_random", "rt_scene_set_box_colors",
+    "rt_debug_timeline", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
 ]
 
 
@@ -159,6 +159,8 @@ def lib():
         L.rt_frame_unpack_shards_rgb8.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32]
         L.rt_scene_load.argtypes = [C.c_char_p, C.POINTER(SceneOpts), C.POINTER(vp)]
         L.rt_box_colors_random.argtypes = [C.c_int32, C.POINTER(RandState), vp]
+        L.rt_frame_shard_tiles.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp]
+        L.rt_frame_shard_tiles.restype = C.c_int32
         L.rt_scene_set_box_colors.argtypes = [vp, vp]
         _lib = L
     return _lib
@@ -498,6 +500,22 @@ class Rand:
 
     def __call__(self):
         return lib().rt_rand(C.byref(self.st))
+
+
+def shard_tiles(W, H, k, n):
+    """rt_frame_shard_tiles: the (tile x, tile y) 16x16 tiles shard k of n renders, in slot order."""
+    m = lib().rt_frame_shard_tiles(W, H, k, n, None)
+    out = np.zeros((max(m, 1), 2), np.int32)
+    lib().rt_frame_shard_tiles(W, H, k, n, _p(out))
+    return [tuple(map(int, t)) for t in out[:m]]
+
+
+def shard_mask(W, H, k, n):
+    """[H, W] bool: the pixels shard k of n renders."""
+    m = np.zeros((H, W), bool)
+    for tx, ty in shard_tiles(W, H, k, n):
+        m[ty * 16:ty * 16 + 16, tx * 16:tx * 16 + 16] = True
+    return m
 
 
 def box_colors_random(n_boxes, rng=None):

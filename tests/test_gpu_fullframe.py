@@ -113,19 +113,14 @@ def test_full_frame_matches_committed_digests(rt, scenes, case):
 
 
 def stitch_shards(rt, sc, W, H, n, mode="primary"):
-    """Render the frame as n tile shards (the multi-GPU partition: tile t -> shard t % n) and stitch."""
+    """Render the frame as n tile shards (the multi-GPU partition, rt_frame_shard_tiles) and stitch."""
     rgb = np.full((H, W, 3), np.nan, np.float32)
     face = np.full((H, W), -7, np.int32)
     t = np.full((H, W), np.nan, np.float32)
-    tx = (W + 15) // 16
-    ntiles = tx * ((H + 15) // 16)
     covered = np.zeros((H, W), np.int32)
     for k in range(n):
         prgb, pface, pt = gpu_frame(rt, sc, W, H, mode, shard=(k, n))
-        mask = np.zeros((H, W), bool)
-        for tt in range(k, ntiles, n):
-            x, y = (tt % tx) * 16, (tt // tx) * 16
-            mask[y:y + 16, x:x + 16] = True
+        mask = rt.shard_mask(W, H, k, n)
         covered += mask
         rgb[mask], face[mask], t[mask] = prgb[mask], pface[mask], pt[mask]
     assert (covered == 1).all(), "the shards do not partition the frame"

@@ -130,11 +130,8 @@ def test_soup_shards_stitch_bitwise(rt, soup):
         out = np.full((H, W, 3), np.nan, np.float32)
         for k in range(n):
             part, st = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, shard=(k, n))
-            tiles = np.zeros((H, W), bool)
-            tx = (W + 15) // 16
-            for tt in range(k, tx * ((H + 15) // 16), n):
-                x, y = (tt % tx) * 16, (tt // tx) * 16
-                tiles[y:y + 16, x:x + 16] = True
+            tiles = rt.shard_mask(W, H, k, n)
+            assert st["primary_rays"] == int(tiles.sum())
             out[tiles] = part[tiles]
         assert out.tobytes() == ref.tobytes(), n
 

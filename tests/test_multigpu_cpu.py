@@ -29,7 +29,21 @@ def test_tile_partition_is_exact_cover(WH, n):
             seen[t] = r
     assert len(seen) == ((W + 15) // 16) * ((H + 15) // 16)
     counts = np.bincount(list(seen.values()), minlength=n)
-    assert counts.max() - counts.min() <= 1  # interleaving balances tile counts
+    S = bench.SHARD_SUPER_TILE if n > 1 else 1
+    assert counts.max() - counts.min() <= S * S  # interleaving super-tiles balances tile counts
+
+
+@pytest.mark.parametrize("WH", [(1920, 1080), (3840, 2160), (1000, 600), (37, 11), (8, 8)])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_shard_tiles_match_library(rt, WH, n):
+    """bench.shard_tiles (the host-side restatement) lists exactly the library's tiles, in its slot order,
+    and rt_frame_shard_bytes holds the largest shard's slots."""
+    W, H = WH
+    for r in range(n):
+        assert bench.shard_tiles(W, H, r, n) == rt.shard_tiles(W, H, r, n), (r, n)
+    S = bench.SHARD_SUPER_TILE if n > 1 else 1
+    sx, sy = -(-((W + 15) // 16) // S), -(-((H + 15) // 16) // S)
+    assert rt.shard_bytes(W, H, n) == -(-(sx * sy) // n) * S * S * 768
 
 
 def test_default_frames_are_baseline_configs():
