@@ -452,7 +452,8 @@ def main():
                                    + (f", split over {n} GPUs" if n > 1 else "")
                                    + (f", REHEARSAL: shard 0 of {K} on one GPU (value = that shard's rate)" if K else ""),
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
-                       "parallelism": f"tiles/{n} (16x16 tiles interleaved over ranks, scene replicated)",
+                       "parallelism": (f"tiles/{n} (64x64-pixel super-tiles interleaved over ranks, scene replicated)"
+                                       if n > 1 else "tiles/1 (one GPU, whole frame)"),
                        "frames_in_flight": info_fif,
                        # per-frame latency with frames in flight (first kernel start to last kernel end of one
                        # frame; frames overlap, so ms_per_step is the throughput interval) and alone
