@@ -1217,6 +1217,9 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #ifndef RT_FULL_OCT_PRIMARY
 #define RT_FULL_OCT_PRIMARY 1
 #endif
+#ifndef RT_FULL_OCT_SHADOW
+#define RT_FULL_OCT_SHADOW 1
+#endif
 // RT_FULL_LANE_K > 0: a secondary packet with at most K active lanes walks per lane (traverse_lane)
 // instead of as a packet (A/B knob)
 #ifndef RT_FULL_LANE_K
@@ -1320,7 +1323,7 @@ __device__ __forceinline__ float clamp01(float x) { return smax(smin(x, 1.0f), 0
 
 // calculateColor (flyscene.cpp:603-614). SHADOWS: per light, a wave-packet any-hit traversal from
 // P + 0.003 L (box predicate from P) decides whether the light contributes (calcSingleColor :543).
-template <bool SHADOWS, bool STATS, int TRAV>
+template <bool SHADOWS, bool STATS, int TRAV, bool OCTSH = false>
 __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, const HitInfo& hi, f3 o, bool lane_hit,
                                          WaveLds<TRAV, STATS>* lds, int wv, uint32_t* cnt) {
   f3 sum{0.0f, 0.0f, 0.0f};
@@ -1337,7 +1340,8 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       setup_cull(sr);
       Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if (STATS && lane_hit) cnt[ST_TOTAL]++;
-      trace_full_ray<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
+      if (OCTSH) trace_oct<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
+      else trace_full_ray<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
     }
     f3 c{0.0f, 0.0f, 0.0f};
     if (lane_hit && !blocked) c = phong(P, st, hi, o, L, lt.c);
@@ -1861,7 +1865,9 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
     hi0.p = f3{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
     hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
   }
-  const f3 direct0 = calc_color<true, STATS, TRAV>(P, st, hi0, r.o, hit0, &lds, wv, cnt);
+  // the primary hits' shadow packets head for the same light from neighbouring points: octant loops for
+  // them too (A/B knob RT_FULL_OCT_SHADOW); the reflection hits' shadows keep the generic loop
+  const f3 direct0 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW != 0>(P, st, hi0, r.o, hit0, &lds, wv, cnt);
   if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
 
   // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
