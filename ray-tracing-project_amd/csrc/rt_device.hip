@@ -1220,6 +1220,12 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #ifndef RT_FULL_OCT_SHADOW
 #define RT_FULL_OCT_SHADOW 1
 #endif
+#ifndef RT_FULL_OCT_SHADOW2  // the reflection hits' shadow packets through trace_oct too
+#define RT_FULL_OCT_SHADOW2 0
+#endif
+#ifndef RT_FULL_OCT_REFL  // the reflection packet through trace_oct (octant loops when its rays share one)
+#define RT_FULL_OCT_REFL 1
+#endif
 // RT_FULL_LANE_K > 0: a secondary packet with at most K active lanes walks per lane (traverse_lane)
 // instead of as a packet (A/B knob)
 #ifndef RT_FULL_LANE_K
@@ -1880,7 +1886,8 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   setup_cull(rr);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  trace_full_ray<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
+  if (RT_FULL_OCT_REFL) trace_oct<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
+  else trace_full_ray<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
   hi1.mat = -1;
@@ -1892,7 +1899,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
     hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
     hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
   }
-  const f3 direct1 = calc_color<true, STATS, TRAV>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
+  const f3 direct1 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW2 != 0>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
   if (hit1) {
     if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
     // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
