@@ -1221,7 +1221,7 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #define RT_FULL_OCT_SHADOW 1
 #endif
 #ifndef RT_FULL_OCT_SHADOW2  // the reflection hits' shadow packets through trace_oct too
-#define RT_FULL_OCT_SHADOW2 0
+#define RT_FULL_OCT_SHADOW2 1
 #endif
 #ifndef RT_FULL_OCT_REFL  // the reflection packet through trace_oct (octant loops when its rays share one)
 #define RT_FULL_OCT_REFL 1
