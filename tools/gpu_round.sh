@@ -28,7 +28,7 @@ for s in $STEPS; do
     c2c5)
       for cfg in "bunny primary" "bunny full" "soup full"; do
         set -- $cfg
-        timeout -k 10 300 python bench.py --scene $1 --mode $2 --no-cpu --steps 20 --warmup 5 \
+        timeout -k 10 300 python bench.py --scene $1 --mode $2 --no-cpu --steps 100 --warmup 5 \
             > $OUT/bench_$1_$2.json 2> $OUT/bench_$1_$2.err
         rc=$?; echo "$1 $2 rc=$rc"; hard $rc
       done ;;
