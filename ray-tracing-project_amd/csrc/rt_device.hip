@@ -1166,7 +1166,7 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
 #ifndef RT_OCT_SPECIALIZE
 #define RT_OCT_SPECIALIZE 1
 #endif
-template <bool ANY, bool STATS, int TRAV>
+template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false>
 __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                           WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   if (RT_OCT_SPECIALIZE && (TRAV == TRAV_B2_LDS || TRAV == TRAV_B2_VGPR)) {
@@ -1200,6 +1200,11 @@ __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool 
       }
     }
   }
+  // mixed-octant packets of divergent secondary rays: one walk per lane (LANE_MIXED, FULL A/B knob)
+  if (LANE_MIXED && !STATS && TRAV == TRAV_B2_LDS) {
+    traverse_lane<ANY, false>(P, r, active, h, found, cnt);
+    return;
+  }
   trace<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
 }
 template <bool STATS, int TRAV>
@@ -1222,6 +1227,9 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #endif
 #ifndef RT_FULL_OCT_SHADOW2  // the reflection hits' shadow packets through trace_oct too
 #define RT_FULL_OCT_SHADOW2 1
+#endif
+#ifndef RT_FULL_MIXED_LANE  // FULL secondary packets whose rays span octants walk per lane (traverse_lane)
+#define RT_FULL_MIXED_LANE 0
 #endif
 #ifndef RT_FULL_OCT_REFL  // the reflection packet through trace_oct (octant loops when its rays share one)
 #define RT_FULL_OCT_REFL 1
@@ -1346,7 +1354,7 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       setup_cull(sr);
       Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if (STATS && lane_hit) cnt[ST_TOTAL]++;
-      if (OCTSH) trace_oct<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
+      if (OCTSH) trace_oct<true, STATS, TRAV, RT_FULL_MIXED_LANE != 0>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
       else trace_full_ray<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
     }
     f3 c{0.0f, 0.0f, 0.0f};
@@ -1886,7 +1894,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   setup_cull(rr);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  if (RT_FULL_OCT_REFL) trace_oct<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
+  if (RT_FULL_OCT_REFL) trace_oct<false, STATS, TRAV, RT_FULL_MIXED_LANE != 0>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   else trace_full_ray<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
