@@ -280,9 +280,11 @@ int rt_frame_download_rgb8(rt_scene* s, int64_t capacity_pixels, uint8_t* rgb8, 
  * other streams (the library's streams do not synchronise with the legacy default stream). */
 int64_t rt_frame_shard_bytes(int32_t width, int32_t height, int32_t shard_count);
 /* The 16x16 tiles shard shard_index of shard_count renders, in its slot order (the order of its packed
- * slice; slots of super-tile tiles outside the frame are skipped here and zero in the slice): tiles_xy
- * [n][2] = (tile x, tile y), NULL = count only. Returns n. */
-int32_t rt_frame_shard_tiles(int32_t width, int32_t height, int32_t shard_index, int32_t shard_count, int32_t* tiles_xy);
+ * slice; slots of super-tile tiles outside the frame are skipped here and zero in the slice): writes the
+ * first min(n, capacity) as tiles_xy [..][2] = (tile x, tile y) (NULL = count only) and returns n, the
+ * shard's tile count (0 for invalid arguments). */
+int32_t rt_frame_shard_tiles(int32_t width, int32_t height, int32_t shard_index, int32_t shard_count, int32_t* tiles_xy,
+                             int32_t capacity);
 int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device);
 int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t shard_count, int32_t width, int32_t height,
                                 void* frame_device, int32_t device);

@@ -3288,7 +3288,8 @@ extern "C" int64_t rt_frame_shard_bytes(int32_t W, int32_t H, int32_t shard_coun
   return (int64_t)shard_tile_slots((W + 15) / 16, (H + 15) / 16, frame_super_tile(shard_count), 0, shard_count) * 768;
 }
 
-extern "C" int32_t rt_frame_shard_tiles(int32_t W, int32_t H, int32_t shard_index, int32_t shard_count, int32_t* tiles_xy) {
+extern "C" int32_t rt_frame_shard_tiles(int32_t W, int32_t H, int32_t shard_index, int32_t shard_count, int32_t* tiles_xy,
+                                        int32_t capacity) {
   if (W <= 0 || H <= 0 || shard_count <= 0 || shard_index < 0 || shard_index >= shard_count) return 0;
   const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16, S = frame_super_tile(shard_count);
   const int slots = shard_tile_slots(tiles_x, tiles_y, S, shard_index, shard_count);
@@ -3297,7 +3298,7 @@ extern "C" int32_t rt_frame_shard_tiles(int32_t W, int32_t H, int32_t shard_inde
     int tx, ty;
     shard_tile_xy(tiles_x, S, shard_index, shard_count, L, tx, ty);
     if (tx >= tiles_x || ty >= tiles_y) continue;
-    if (tiles_xy) { tiles_xy[2 * n] = tx; tiles_xy[2 * n + 1] = ty; }
+    if (tiles_xy && n < capacity) { tiles_xy[2 * n] = tx; tiles_xy[2 * n + 1] = ty; }
     n++;
   }
   return n;

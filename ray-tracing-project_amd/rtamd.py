@@ -159,7 +159,7 @@ def lib():
         L.rt_frame_unpack_shards_rgb8.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32]
         L.rt_scene_load.argtypes = [C.c_char_p, C.POINTER(SceneOpts), C.POINTER(vp)]
         L.rt_box_colors_random.argtypes = [C.c_int32, C.POINTER(RandState), vp]
-        L.rt_frame_shard_tiles.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp]
+        L.rt_frame_shard_tiles.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32]
         L.rt_frame_shard_tiles.restype = C.c_int32
         L.rt_scene_set_box_colors.argtypes = [vp, vp]
         _lib = L
@@ -504,9 +504,9 @@ class Rand:
 
 def shard_tiles(W, H, k, n):
     """rt_frame_shard_tiles: the (tile x, tile y) 16x16 tiles shard k of n renders, in slot order."""
-    m = lib().rt_frame_shard_tiles(W, H, k, n, None)
+    m = lib().rt_frame_shard_tiles(W, H, k, n, None, 0)
     out = np.zeros((max(m, 1), 2), np.int32)
-    lib().rt_frame_shard_tiles(W, H, k, n, _p(out))
+    lib().rt_frame_shard_tiles(W, H, k, n, _p(out), m)
     return [tuple(map(int, t)) for t in out[:m]]
 
 

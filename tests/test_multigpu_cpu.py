@@ -44,6 +44,12 @@ def test_shard_tiles_match_library(rt, WH, n):
     S = bench.SHARD_SUPER_TILE if n > 1 else 1
     sx, sy = -(-((W + 15) // 16) // S), -(-((H + 15) // 16) // S)
     assert rt.shard_bytes(W, H, n) == -(-(sx * sy) // n) * S * S * 768
+    # a smaller buffer receives only its capacity
+    import ctypes
+    full = rt.shard_tiles(W, H, 0, n)
+    buf = (ctypes.c_int32 * 4)(*([-1] * 4))
+    assert rt.lib().rt_frame_shard_tiles(W, H, 0, n, ctypes.cast(buf, ctypes.c_void_p), 1) == len(full)
+    assert list(buf) == [full[0][0], full[0][1], -1, -1]
 
 
 def test_default_frames_are_baseline_configs():
