@@ -169,6 +169,15 @@ __device__ __forceinline__ void setup_cull(Ray& r) {
   r.oid = f3{-r.o.x * r.id.x, -r.o.y * r.id.y, -r.o.z * r.id.z};
 }
 
+#ifndef RT_TRI_VREG  // edge differences from VGPR copies of w0 / w1 (fewer moves)
+#define RT_TRI_VREG 1
+#endif
+#ifndef RT_EYE_VREG  // k_primary_fused keeps the eye in VGPRs
+#define RT_EYE_VREG 1
+#endif
+#ifndef RT_PK_SLAB  // octant slabs as v_pk_fma_f32 over the (lo, hi) coordinate pairs
+#define RT_PK_SLAB 0
+#endif
 // Conservative slab test for one padded child box (culling only; exactness comes from padding):
 // returns the entry distance tmin and the exit distance clipped to [0, tmax_ray] (hit iff tmin <= tmax)
 struct Span {
@@ -195,6 +204,30 @@ template <int OCT>
 __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
                                        float tmax_ray) {
   if (OCT < 0) return slab(lx, hx, ly, hy, lz, hz, r, tmax_ray);
+#if RT_PK_SLAB
+  {
+    // both planes of an axis in one packed fma: the record's (lo, hi) pair is an aligned SGPR pair, the
+    // ray's id / oid are held pairwise as (id.x, id.y), (id.z, oid.x), (oid.y, oid.z) and broadcast by
+    // op_sel (each half rounded once, as v_fma_f32)
+    auto pk = [](float a, float b) { return ((uint64_t)__float_as_uint(b) << 32) | __float_as_uint(a); };
+    const uint64_t pa = pk(r.id.x, r.id.y), pb = pk(r.id.z, r.oid.x), pc = pk(r.oid.y, r.oid.z);
+    uint64_t tx, ty, tz;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tx) : "s"(pk(lx, hx)), "v"(pa), "v"(pb));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(ty) : "s"(pk(ly, hy)), "v"(pa), "v"(pc));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tz) : "s"(pk(lz, hz)), "v"(pb), "v"(pc));
+    const float tx0 = __uint_as_float((uint32_t)tx), tx1 = __uint_as_float((uint32_t)(tx >> 32));
+    const float ty0 = __uint_as_float((uint32_t)ty), ty1 = __uint_as_float((uint32_t)(ty >> 32));
+    const float tz0 = __uint_as_float((uint32_t)tz), tz1 = __uint_as_float((uint32_t)(tz >> 32));
+    const float nx = (OCT & 1) ? tx1 : tx0, fx = (OCT & 1) ? tx0 : tx1;
+    const float ny = (OCT & 2) ? ty1 : ty0, fy = (OCT & 2) ? ty0 : ty1;
+    const float nz = (OCT & 4) ? tz1 : tz0, fz = (OCT & 4) ? tz0 : tz1;
+    Span s;
+    // (as asm: the compiler would canonicalise the asm-produced planes with an extra v_max each)
+    asm("v_max_f32 %0, 0, %3\n\tv_max3_f32 %0, %1, %2, %0" : "=&v"(s.tmin) : "v"(nx), "v"(ny), "v"(nz));
+    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(s.tmax) : "v"(fx), "v"(fy), "v"(fz), "v"(tmax_ray));
+    return s;
+  }
+#endif
   const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
   const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
   const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
@@ -291,7 +324,15 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
   if (cand == 0) return;
   const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
+#if RT_TRI_VREG
+  // the record is wave-uniform (SGPRs) and a VALU op reads at most one SGPR: w0 and w1 copied into
+  // VGPRs once serve all three edge differences (6 moves instead of 9; same float operations)
+  f3 v0 = w0, v1 = w1;
+  asm("" : "+v"(v0.x), "+v"(v0.y), "+v"(v0.z), "+v"(v1.x), "+v"(v1.y), "+v"(v1.z));
+  const f3 e0 = sub(w1, v0), e1 = sub(w2, v1), e2 = sub(v0, w2);
+#else
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
+#endif
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
   cand &= ~ballot((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0));
   if (cand == 0) return;
@@ -1799,7 +1840,14 @@ void k_primary_fused(FrameParams P) {
   __shared__ WaveLds<TRAV_B2_LDS, false> lds;
   wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<RT_TRACE_WPB>(P);
+#if RT_EYE_VREG
+  // the eye (every primary ray's origin) held in VGPRs: origin.dot(facenormal) in each triangle test
+  // then reads one SGPR per op and needs no moves
+  Ray r = primary_ray(P, c.px, c.py);
+  asm("" : "+v"(r.o.x), "+v"(r.o.y), "+v"(r.o.z));
+#else
   const Ray r = primary_ray(P, c.px, c.py);
+#endif
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
   if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
