@@ -160,7 +160,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
     return RT_ERR_IO;
   }
   if (h.nv < 0 || h.nf < 0 || h.n_mats < 0 || h.n_boxes < 0 || h.n_box_faces != h.nf || h.n_nodes < 0 ||
-      h.n_nodes4 < 0 || h.n_tris != h.nf) {
+      h.n_nodes4 < 0 || h.n_tris < h.nf || (int64_t)h.n_tris > 2 * (int64_t)h.nf + 1) {  // SBVH: references >= faces
     rt::set_error("rt_scene_load: inconsistent header in %s", path);
     return RT_ERR_IO;
   }

@@ -160,7 +160,9 @@ def _soup(rt, n, seed=3, scale=1.0, flat_axis=None):
                                   "coincident", "single", "two"])
 def test_bvh_trees_sound(rt, case):
     """Binary and 4-wide trees: every triangle inside every ancestor box (the wide boxes dequantised
-    exactly as the kernel does), every triangle record in exactly one leaf; depth fits the stacks."""
+    exactly as the kernel does) -- for a spatial-split tree every reference's part inside its path's
+    boxes and every face covered by its leaves' regions --, every triangle record in exactly one leaf;
+    depth fits the stacks."""
     if case in ("cube", "dodgeColorTest", "bunny"):
         mesh = rt.Mesh.load_obj(scene_path(case + ".obj"))
     elif case == "soup200k":
@@ -181,7 +183,9 @@ def test_bvh_trees_sound(rt, case):
     r = sc.validate_bvh()
     assert r["ok"] and r["violations"] == 0, r
     nf = sc.info()["n_faces"]
-    assert r["covered2"] == nf and r["covered4"] == nf
+    # every triangle record in exactly one leaf; spatial splits may reference a face from several leaves
+    # (the validator then checks that the faces' leaf regions cover them), within the reference budget
+    assert nf <= r["covered2"] <= 1.5 * nf + 1 and r["covered4"] == r["covered2"]
     assert r["nodes4"] >= 1 and r["depth4"] <= r["depth2"] and 3 * r["depth4"] + 4 <= 128
 
 
