@@ -730,6 +730,13 @@ struct Aabb {
   }
 };
 
+// one more concurrent subtree task if fewer than `cap` run (the build order and result do not depend on it)
+static bool take_task(std::atomic<int>& live, unsigned cap) {
+  if (live.fetch_add(1) < (int)cap) return true;
+  live.fetch_sub(1);
+  return false;
+}
+
 // Binned SAH over the working array of primitives (partitioned in place, so a subtree's primitives are
 // contiguous and become the leaf order). Large ranges bin and bound in parallel chunks (min/max/count
 // merges are order-independent, so the splits do not depend on the thread count); subtrees above
@@ -742,6 +749,9 @@ struct BvhBuilder {
   float pad;
   unsigned hw = 1;
   std::atomic<int> max_depth{0}, leaves{0};
+  // concurrent subtree tasks of this build, at most hw (a torchrun job builds one scene per rank on the
+  // same host: without a bound each rank would start ~250 threads at once)
+  std::atomic<int> tasks{0};
   static constexpr int kBins = 32;
   static constexpr float kIsect = 1.0f;
   // node-visit cost relative to one triangle test (RT_SAH_TRAV, A/B knob). 0.7: once the packet node
@@ -873,10 +883,11 @@ struct BvhBuilder {
     const uint32_t me = next.fetch_add(1);
     Aabb lb, rb;
     uint32_t lh, rh;
-    if (n > 4096 && depth < 16) {
+    if (n > 4096 && depth < 16 && take_task(tasks, hw)) {
       auto fut = std::async(std::launch::async, [&]() { return build(b, mid, depth + 1, lb); });
       rh = build(mid, e, depth + 1, rb);
       lh = fut.get();
+      tasks.fetch_sub(1);
     } else {
       lh = build(b, mid, depth + 1, lb);
       rh = build(mid, e, depth + 1, rb);
@@ -905,6 +916,7 @@ struct SbvhBuilder {
   int leaf_size = 4;
   float pad = 0.0f, kTrav = 0.7f, alpha = 1e-5f, root_area = 1.0f;
   std::atomic<int> max_depth{0};
+  std::atomic<int> tasks{0};  // concurrent subtree tasks, at most hw (as BvhBuilder)
   static constexpr int kBins = 32;
   static constexpr float kIsect = 1.0f;
 
@@ -1164,10 +1176,11 @@ struct SbvhBuilder {
     const uint32_t me = next.fetch_add(1);
     Aabb lb, rb;
     uint32_t lh, rh;
-    if (n > 4096 && depth < 16) {
+    if (n > 4096 && depth < 16 && take_task(tasks, hw)) {
       auto fut = std::async(std::launch::async, [&]() { return build(L, depth + 1, lb); });
       rh = build(R, depth + 1, rb);
       lh = fut.get();
+      tasks.fetch_sub(1);
     } else {
       lh = build(L, depth + 1, lb);
       rh = build(R, depth + 1, rb);
