@@ -364,6 +364,12 @@ int rt_debug_set_variant(int32_t v);
  * that frame; capacity_waves smaller than that -> RT_ERR_INVALID. */
 int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64_t* n_waves);
 
+/* Raw counters of the last RT_FRAME_STATS frame (diagnostics), out[0..n): 0 node visits, 1 triangle tests,
+ * 2 wave node fetches, 3 wave triangle fetches, 4 primary rays, 5 hits, 6 total rays, 7 wave stack pops,
+ * 8 pops at which no lane that wanted the entry still could reach it before its closest hit (closest-hit
+ * traversal only); entries past the last counter are 0. */
+int rt_debug_counters(rt_scene* s, int64_t n, int64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -147,7 +147,11 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_bal
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
 // counters of the RT_FRAME_STATS counting run
-enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_COUNT };
+// ST_WPOP / ST_WCULL (counting run, closest hit): stack pops per wave, and those pops at which no lane
+// that wanted the entry still could (every such lane's entry distance into it, recorded at the push,
+// now beyond its closest hit) -- what culling at the pop would save (rt_debug_counters)
+enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_COUNT };
+constexpr int kStatSlots = 16;
 
 struct Hit {
   float t;
@@ -420,6 +424,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
   uint32_t stackv = 0;     // lane k holds stack entry k (VGPR stack)
   int sp = 0;              // wave-uniform stack depth (SGPR)
   uint64_t flagstack = 0;  // STATS: per-lane "my ray wanted this entry" bit per stack level
+  float tstack[STATS ? 64 : 1];  // STATS: per-lane entry distance into each stack entry
   bool want = active;      // STATS: this lane's ray intersects the current node
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
@@ -480,6 +485,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
         const bool wf = first0 ? h1 : h0;
         flagstack = (flagstack & ~(1ull << sp)) | ((uint64_t)wf << sp);
         want = first0 ? h0 : h1;
+        tstack[sp] = first0 ? s1.tmin : s0.tmin;
       }
       sp += ((m0 != 0) & (m1 != 0)) ? 1 : 0;
       node = first0 ? nd.child0 : nd.child1;
@@ -511,7 +517,11 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       if (sp == 0) break;
       sp--;
       node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
-      if (STATS) want = (flagstack >> sp) & 1;
+      if (STATS) {
+        want = (flagstack >> sp) & 1;
+        cnt[ST_WPOP]++;
+        if (!ANY && ballot(want && tstack[sp] <= h.t) == 0) cnt[ST_WCULL]++;
+      }
     }
   }
 }
@@ -1527,7 +1537,7 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
 #pragma unroll
   for (int c = 0; c < ST_COUNT; c++) {
     unsigned long long v = cnt[c];
-    if (c == ST_WNODE || c == ST_WTRI) v = (lane == 0) ? v : 0;  // wave fetches counted once
+    if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL) v = (lane == 0) ? v : 0;  // wave counts once
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(P.stats + c, v);
   }
@@ -1612,7 +1622,7 @@ __global__ __launch_bounds__(64 * RT_TRACE_WPB) __attribute__((amdgpu_waves_per_
 void k_trace_primary(FrameParams P) {
   __shared__ WaveLds<TRAV, STATS> lds;
   const PixelCoord c = pixel_coord<RT_TRACE_WPB>(P);
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[ST_COUNT] = {};
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && c.active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -2057,7 +2067,7 @@ void k_render_full(FrameParams P) {
   wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<RT_FULL_WPB>(P);
   const bool active = c.active;
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[ST_COUNT] = {};
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
 
@@ -2098,7 +2108,7 @@ void k_render_depth(FrameParams P) {
   wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<1>(P);
   const bool active = c.active;
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[ST_COUNT] = {};
   Ray cur = primary_ray(P, c.px, c.py);
   const Ray r0 = cur;
   if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
@@ -2297,7 +2307,7 @@ void k_full_shadow(FrameParams P, int pass) {
   const uint32_t pix = L.act ? (pass ? P.list1 : P.list0)[L.i] : 0u;
   const HitState hs = (pass ? P.state1 : P.state0)[pix];
   const f3 p{hs.px, hs.py, hs.pz};
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[ST_COUNT] = {};
   uint32_t bits = 0;
   for (int l = 0; l < P.n_lights; l++) {
     const f3 Ld = light_dir(p, frame_light(l));
@@ -2337,7 +2347,7 @@ void k_full_refl(FrameParams P) {
   rr.o2 = affv3(P.Minv, rr.o);
   rr.d2 = normalized(m3v3(P.MS, rr.d));
   setup_cull(rr);
-  uint32_t cnt[ST_COUNT] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[ST_COUNT] = {};
   if (STATS && L.act) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
@@ -2675,7 +2685,7 @@ int device_upload(rt_scene* s) {
     d.ns = hs.mats[m].shininess;
   }
   if ((rc = dalloc_copy(&s->d_mats, dm.data(), dm.size() * sizeof(DevMat), tot))) return rc;
-  if ((rc = dalloc_copy(&s->d_stats, nullptr, 8 * sizeof(unsigned long long), tot))) return rc;
+  if ((rc = dalloc_copy(&s->d_stats, nullptr, kStatSlots * sizeof(unsigned long long), tot))) return rc;
   return RT_OK;
 }
 
@@ -2926,6 +2936,19 @@ extern "C" int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* 
   return RT_OK;
 }
 
+extern "C" int rt_debug_counters(rt_scene* s, int64_t n, int64_t* out) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  if (!out || n < 0) { set_error("rt_debug_counters: no output"); return RT_ERR_INVALID; }
+  if (!(s->last_flags & RT_FRAME_STATS)) { set_error("rt_debug_counters: last frame had no RT_FRAME_STATS"); return RT_ERR_INVALID; }
+  HIPCHECK(hipSetDevice(s->device));
+  HIPCHECK(hipDeviceSynchronize());
+  unsigned long long c[kStatSlots];
+  HIPCHECK(hipMemcpy(c, s->d_stats, sizeof c, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < n; i++) out[i] = i < ST_COUNT ? (int64_t)c[i] : 0;
+  return RT_OK;
+}
+
 extern "C" int rt_debug_set_variant(int32_t v) {
   const int prev = kernel_variant();
   g_variant.store(v < 0 ? 0 : v);
@@ -3035,7 +3058,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     // the counters are shared: a counting frame waits for every frame in flight on the other slots
     for (int k = 0; k < s->n_slots; k++)
       if (k != slot_id && s->slots[k].last_done) HIPCHECK(hipStreamWaitEvent(st, (hipEvent_t)s->slots[k].last_done, 0));
-    HIPCHECK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st));
+    HIPCHECK(hipMemsetAsync(s->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
   }
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
@@ -3264,7 +3287,7 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
     out->primary_rays = s->last_rays;
     out->total_rays = s->last_rays;
     if (s->last_flags & RT_FRAME_STATS) {
-      unsigned long long c[8];
+      unsigned long long c[kStatSlots];
       HIPCHECK(hipMemcpy(c, s->d_stats, sizeof c, hipMemcpyDeviceToHost));
       out->node_visits = (int64_t)c[ST_NODE];
       out->tri_tests = (int64_t)c[ST_TRI];

@@ -31,7 +31,7 @@ EXPORTS = [
     "rt_frame_download_rgb8", "rt_write_ppm_rgb8", "rt_frame_shard_bytes", "rt_frame_pack_shard_rgb8",
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
-    "rt_debug_timeline", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
+    "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
 ]
 
 
@@ -138,6 +138,7 @@ def lib():
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
         L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
+        L.rt_debug_counters.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
         L.rt_frame_download_rgb8.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
@@ -316,6 +317,12 @@ class Scene:
         t = np.zeros((H, W), np.float32) if want_hits else None
         check(lib().rt_frame_download(self.h, W * H, _p(rgb), _p(face), _p(t)))
         return (rgb, face, t) if want_hits else rgb
+
+    def counters(self, n=16):
+        """Raw counters of the last RT_FRAME_STATS frame (rt_debug_counters): int64 [n]."""
+        out = (C.c_int64 * n)()
+        check(lib().rt_debug_counters(self.h, n, out))
+        return [int(x) for x in out]
 
     def timeline(self):
         """Per-wave records of the last RT_FRAME_TIMELINE frame: uint32 [n_waves, 8] (rt_debug_timeline)."""

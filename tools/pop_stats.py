@@ -1,0 +1,39 @@
+"""Counting run of the C3 soup / bunny frames (RT_FRAME_STATS) and the raw counters of rt_debug_counters:
+how many wave stack pops there are per wave, and how many of them no lane still needed (every lane that
+had wanted the entry now has a closest hit nearer than its entry distance) -- the node steps that a
+culling test at the pop would save. Usage: python tools/pop_stats.py [soup|bunny ...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import conftest  # noqa: E402
+
+rt = conftest.rtamd
+NAMES = ["node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "primary_rays", "hits",
+         "total_rays", "wave_pops", "wave_pops_cullable"]
+
+
+def main(scenes):
+    W, H = 1920, 1080
+    for name in scenes:
+        if name == "soup":
+            mesh, _, _ = rt.soup_mesh(1_000_000, 12345)
+        else:
+            mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
+        sc = rt.Scene(mesh, device=0)
+        sc.render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS)
+        out = sc.counters()
+        d = {k: out[i] for i, k in enumerate(NAMES)}
+        waves = (W // 8) * ((H + 7) // 8)
+        d["scene"] = name
+        d["waves"] = waves
+        d["pops_per_wave"] = d["wave_pops"] / waves
+        d["node_steps_per_wave"] = d["wave_node_fetches"] / waves
+        d["cullable_share_of_pops"] = d["wave_pops_cullable"] / max(d["wave_pops"], 1)
+        print(json.dumps(d), flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["soup", "bunny"])
