@@ -115,7 +115,8 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
     out["tag"] = tag
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc.json")
     json.dump(out, open(path, "w"), indent=1)
-    json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_latest.json"), "w"), indent=1)
+    if os.environ.get("RT_PROFILE_LATEST", "1") != "0":  # 0: a side profile (not the bench workload's)
+        json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_latest.json"), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "bench_line_under_trace"}, indent=1))
 
 
