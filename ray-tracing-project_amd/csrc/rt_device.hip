@@ -1424,6 +1424,7 @@ struct PixelCoord {
   int px, py, wv, lane;
   int slot;   // this wave's LDS slot within its block
   int qw;     // global wave number (tile-block * 4 + wave): the same for every block shape
+  int sub;    // FrameParams::split_k: this block's 16-lane part (rows 2 sub, 2 sub + 1) of its wave, else -1
   bool active;
 };
 
@@ -1438,12 +1439,25 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   c.lane = threadIdx.x & 63;
   int nb, b;
   int bid = (int)blockIdx.x;
+  c.sub = -1;
   if (RT_ORDER_LPT && WPB == 1 && P.order != nullptr) {
     // longest-first order from an earlier frame's wave costs (k_order_lpt): a permutation of the
     // logical waves that keeps each XCD on its own chunked bands; an out-of-range entry (never
-    // produced) falls back to the block's own id, so a wave never leaves the grid
-    const uint32_t o = uniform(P.order[blockIdx.x]);
-    bid = o < gridDim.x ? (int)o : (int)blockIdx.x;
+    // produced) falls back to the block's own position, so a wave never leaves the grid.
+    // split_k > 0: order positions 0 .. split_k - 1 (the costliest waves) are traced by four blocks
+    // each, every one with 16 of the wave's lanes, so the frame's slowest packets shrink to 16 rays
+    const uint32_t k = (uint32_t)P.split_k, nlog = gridDim.x - 3u * k;
+    uint32_t pos = blockIdx.x;
+    if (k > 0) {
+      if (pos < 4u * k) {
+        c.sub = (int)(pos & 3u);
+        pos >>= 2;
+      } else {
+        pos -= 3u * k;
+      }
+    }
+    const uint32_t o = uniform(P.order[pos]);
+    bid = o < nlog ? (int)o : (int)pos;
   } else if (P.xcd_remap >= 2) {
     // chunked XCD order: blocks b and b + 8 share an XCD, so the k-th block of XCD x takes position
     // (k / C) * 8C + x C + k % C -- each XCD receives runs of C consecutive blocks (for one-wave
@@ -1463,7 +1477,7 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   } else {
     c.wv = bid & 3;
     c.slot = 0;
-    nb = (int)(gridDim.x >> 2);
+    nb = (int)((gridDim.x - 3u * (uint32_t)P.split_k) >> 2);
     b = bid >> 2;
   }
   c.qw = b * 4 + c.wv;
@@ -1476,7 +1490,7 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
   shard_tile_xy(P.tiles_x, P.super_tile, P.shard_index, P.shard_count, L, tx, ty);
   c.px = tx * 16 + (c.wv & 1) * 8 + (c.lane & 7);
   c.py = ty * 16 + (c.wv >> 1) * 8 + (c.lane >> 3);
-  c.active = c.px < P.W && c.py < P.H;
+  c.active = c.px < P.W && c.py < P.H && (c.sub < 0 || (c.lane >> 4) == c.sub);
   return c;
 }
 
@@ -1513,13 +1527,17 @@ __device__ __forceinline__ void wave_clock_start(const FrameParams& P, uint32_t*
     }
   }
 }
-__device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint32_t* clk, int lane, int qw) {
+__device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint32_t* clk, int lane, int qw,
+                                               bool keep_cost = false) {
   if (!RT_WAVE_CLOCK || (!P.timeline && !P.cost)) return;
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   struct { uint64_t t0; uint32_t r0; } w;
   w.t0 = (uint64_t)uniform(clk[0]) | ((uint64_t)uniform(clk[1]) << 32);
   w.r0 = uniform(clk[2]);
-  if (P.cost && lane == 0) {  // this wave's cost for the next frame's dispatch order
+  // this wave's cost for the next frame's dispatch order; a split sub-wave leaves the whole wave's cost
+  // from an earlier frame in place (it ranked the wave among the costliest; the sub-wave's own time
+  // would not)
+  if (P.cost && lane == 0 && !keep_cost) {
     const uint64_t dt = t1 - w.t0;
     P.cost[qw] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
   }
@@ -1555,6 +1573,8 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
 // thread places its contiguous run of waves. Any order is a permutation: every frame renders identical
 // bits.
 constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
+constexpr int kSplitK = 2048;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k)
+constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
 __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c, int shift) {
   // 4 buckets per octave: exponent and 2 mantissa bits of (float)c; costs of 2^10 .. 2^18 shader cycles
   // (0.5 .. 120 us at 2.1 GHz) spread over the buckets, longest first (bucket 0)
@@ -1861,7 +1881,7 @@ void k_primary_fused(FrameParams P) {
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
   if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
-  wave_clock_end(P, lds.clk, c.lane, c.qw);
+  wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
 }
 
 // PRIMARY with two 8x8 packets per wave (dual-chain traversal, traverse_dual): block b traces pair b
@@ -2087,7 +2107,7 @@ void k_render_full(FrameParams P) {
     }
   }
   if (STATS) flush_stats(P, cnt, c.lane);
-  wave_clock_end(P, lds.clk, c.lane, c.qw);
+  wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
 }
 
 // traceRay(o, d, 0) for any recursion limit D = P.max_depth (flyscene.cpp:317-371; the reference fixes
@@ -2852,7 +2872,7 @@ static void launch_trace(const FrameParams& P, int grid, hipStream_t st, int tra
 }
 template <bool STATS, bool HITS>
 static void launch_full(const FrameParams& P, int grid, hipStream_t st, int trav, bool small) {
-  const dim3 g(grid * (4 / RT_FULL_WPB)), b(64 * RT_FULL_WPB);
+  const dim3 g(grid * (4 / RT_FULL_WPB) + 3 * P.split_k), b(64 * RT_FULL_WPB);
   if (trav == TRAV_B2_VGPR) hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_VGPR>), g, b, 0, st, P);
   else if (trav == TRAV_B2_LDS && !STATS && small)
     hipLaunchKernelGGL((k_render_full<STATS, HITS, TRAV_B2_LDS, RT_FULL_WAVES_PER_EU_SMALL>), g, b, 0, st, P);
@@ -3178,7 +3198,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipEventRecord(ev_m, st));
     } else if (prim && !stats && !(variant & (32768 | 256 | 2048)) && trav == TRAV_B2_LDS) {
-      const dim3 g(grid * (4 / RT_TRACE_WPB)), b(64 * RT_TRACE_WPB);
+      // lone frames of small scenes: the costliest waves as 16-lane sub-waves, as k_render_full does
+      // (RT_SPLIT_KP waves)
+      static const int split_p = [] { const char* e = getenv("RT_SPLIT_KP"); return e ? atoi(e) : kSplitKPrimary; }();
+      const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
+      P.split_k = (P.order && small_p && !P.timeline && RT_TRACE_WPB == 1)
+                      ? std::max(0, std::min<int>(split_p, (int)(units / 4))) & ~7 : 0;
+      const dim3 g(grid * (4 / RT_TRACE_WPB) + 3 * P.split_k), b(64 * RT_TRACE_WPB);
       // RT_LDS_PAD (diagnostics): extra dynamic LDS per block, to cap the resident waves per CU in
       // occupancy experiments (160 KiB / (pad + 1 KiB) blocks per CU)
       static const unsigned lds_pad = [] { const char* e = getenv("RT_LDS_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
@@ -3219,6 +3245,18 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       // occupancy by scene size (k_render_full); variant bits 8192 / 16384 force the 8-wave / small build
       const size_t rec_bytes = (s->hs.nodes.size() + s->hs.tris.size()) * 64;
       const bool small = (variant & 16384) || (!(variant & 8192) && rec_bytes <= kFullSmallSceneBytes);
+      // a lone frame of a small (L2-resident) scene, dispatched longest-first, splits its costliest waves
+      // into 16-lane sub-waves (FrameParams::split_k; RT_SPLIT_K waves, rounded down to a multiple of 8
+      // and at most a quarter of the frame's waves): such a frame's span is its slowest waves' (C5 one
+      // frame alone: 2.2 resident waves per SIMD on average), and a 16-ray packet of their incoherent
+      // secondary rays finishes sooner. A large scene's FULL frame is not tail bound (5.7 resident waves
+      // per SIMD on the soup) and the extra waves only cost (-6%), so it keeps whole waves. Results do not
+      // depend on the grouping (exact per-lane culling, (t, rank) argmin).
+      static const int split_env = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atoi(e) : kSplitK; }();
+      if (P.order && small && !P.timeline && !stats && RT_FULL_WPB == 1 && trav == TRAV_B2_LDS)
+        P.split_k = std::max(0, std::min<int>(split_env, (int)(units / 4))) & ~7;
+      else
+        P.split_k = 0;
       if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav, small); else launch_full<true, false>(P, grid, st, trav, small); }
       else { if (hits) launch_full<false, true>(P, grid, st, trav, small); else launch_full<false, false>(P, grid, st, trav, small); }
       HIPCHECK(hipEventRecord(ev_m, st));

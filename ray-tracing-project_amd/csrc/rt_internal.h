@@ -189,6 +189,10 @@ struct FrameParams {
   // chunked-XCD order. cost[logical wave] receives the wave's duration in shader cycles (null = off).
   const uint32_t* order;
   uint32_t* cost;
+  // k_render_full with an order: the first split_k logical waves of the order (the costliest of an
+  // earlier frame) run as four 16-lane sub-waves each (blocks 0 .. 4 split_k - 1), the rest whole; the
+  // grid is then (logical waves + 3 split_k) blocks. 0 = off.
+  int32_t split_k;
   const float* face_boxcolor;  // RT_MODE_BOX_COLORS: [n_faces][4] summed box colours per face id
 };
 

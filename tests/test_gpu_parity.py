@@ -527,6 +527,29 @@ def test_longest_first_dispatch_order(rt):
             assert (cls[o] == pos % 8).all()                 # every wave keeps its XCD position class
 
 
+def test_split_costliest_waves(rt, soup):
+    """Lone FULL frames dispatched longest-first trace their costliest waves (FrameParams::split_k) as four
+    16-lane sub-waves each: every frame after a slot's first (which has no wave costs yet) must still
+    render the bits of the default-order frame (variant 131072: no longest-first order, hence no split),
+    for frames large enough to split and for a frame too small to (fewer than 32 waves); the soup (a
+    large scene) keeps whole waves, and with RT_SPLIT_K forced the library reads it once per process, so
+    the soup case checks the unsplit order path."""
+    mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
+    cases = [(rt.Scene(mesh, frames_in_flight=1), 1000, 563), (rt.Scene(mesh, frames_in_flight=1), 24, 16),
+             (soup[0], 480, 270)]
+    for (sc, W, H), mode in [(c, m) for c in cases for m in (rt.RT_MODE_FULL, rt.RT_MODE_PRIMARY)]:
+        cam = rt.flycam(W, H, 0, 0, 20)
+        prev = rt.set_variant(131072)
+        try:
+            ref = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
+        finally:
+            rt.set_variant(prev)
+        for k in range(20):  # past the order's refresh (8 frames per slot) on one slot and on four
+            got = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
+            for a, b in zip(ref[:3], got[:3]):
+                assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (W, H, mode, k)
+
+
 @pytest.mark.parametrize("name", ["cube", "dodgeColorTest", "bunny", "soup"])
 def test_box_colors_mode(rt, orc, soup, name):
     """RT_MODE_BOX_COLORS = traceRay with RENDER_BOUNDINGBOX_COLORED_TRIANGLES set (flyscene.cpp:334-348):
