@@ -462,7 +462,8 @@ def main():
                        "host_enqueue_ms_per_frame": round(st.get("enqueue_ms", 0.0), 4),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
-                       "builder": "lbvh-gpu" if info["builder"] == 1 else "sah-host",
+                       "builder": "lbvh-gpu" if info["builder"] == 1 else (
+                           "sah-host" if os.environ.get("RT_SBVH", "") in ("0", "0.0") else "sbvh-host"),
                        "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
                                     "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),
                                     "upload": round(info["upload_ms"], 1)}, **more},

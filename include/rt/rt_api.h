@@ -101,8 +101,12 @@ typedef struct rt_scene_opts {
   float background[3];    /* Flyscene::BACKGROUND_COLOR (flyscene.hpp:175) */
   int32_t frames_in_flight; /* rt_render_async frames that may execute concurrently (1..4, default 4):
                              * each in-flight frame has its own stream and frame buffers; frames stay
-                             * independent and rt_frame_download returns the most recent one */
-  int32_t builder;          /* RT_BUILDER_SAH (host binned SAH, default: fastest traversal) or
+                             * independent and rt_frame_download returns the most recent one. A frame
+                             * alone on the GPU is dispatched longest-first from an earlier frame's wave
+                             * costs (small scenes also split their costliest waves); results never
+                             * depend on the dispatch order */
+  int32_t builder;          /* RT_BUILDER_SAH (host SAH tree, default: fastest traversal; a spatial-split
+                             * BVH, or the plain binned-SAH tree with the environment variable RT_SBVH=0) or
                              * RT_BUILDER_LBVH_GPU (Morton/radix-sort/Karras build on the
                              * device in milliseconds; falls back to SAH when the tree would be too deep) */
   int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_HOST (default,
