@@ -279,8 +279,11 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + 8-bit frame to host) timing")
     ap.add_argument("--no-extra", action="store_true", help="skip the second frame size (c4_frame / c3_frame)")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
-    ap.add_argument("--builder", choices=["sah", "lbvh"], default="sah",
-                    help="BVH builder: host binned SAH (default) or the device LBVH (SURVEY f2)")
+    ap.add_argument("--builder", choices=["sbvh", "sah", "lbvh"], default="sbvh",
+                    help="BVH builder: host SAH with spatial splits (default), host binned SAH, or the device LBVH "
+                         "(SURVEY f2)")
+    ap.add_argument("--wide", action="store_true",
+                    help="also build the fp32 4-wide tree and walk it for PRIMARY packets (rt_scene_opts.wide_tree)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames that may overlap on the GPU (0 = library default, 4)")
     ap.add_argument("--rehearse-shards", type=int, default=0,
@@ -335,7 +338,8 @@ def main():
         mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         scene_name = "Stanford bunny (69,451 triangles)"
     sc = rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight,
-                  builder=rt.RT_BUILDER_LBVH_GPU if a.builder == "lbvh" else rt.RT_BUILDER_SAH)
+                  builder={"lbvh": rt.RT_BUILDER_LBVH_GPU, "sah": rt.RT_BUILDER_SAH, "sbvh": rt.RT_BUILDER_SBVH}[a.builder],
+                  wide_tree=1 if a.wide else 0)
     info = sc.info()
     info_fif = a.frames_in_flight or 4
     setup_s = time.perf_counter() - t0
@@ -382,7 +386,7 @@ def main():
         kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
         # the packet algorithm's bytes per launch: node / triangle records once per wave, the hit lanes'
         # triangle + shading records, the pixel
-        wave_bytes = 64.0 * (stats["wave_node_fetches"] + stats["wave_tri_fetches"])
+        wave_bytes = float(stats["wave_node_bytes"]) + 64.0 * stats["wave_tri_fetches"]
         alg_bytes = wave_bytes + stats["hits"] * (64 + 48) + 12.0 * rays
         kern_ms = iso_trace_ms if mode == rt.RT_MODE_PRIMARY else iso_ms
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -461,9 +465,9 @@ def main():
                        "kernel_ms_one_frame_alone": round(iso_ms_max, 4),
                        "host_enqueue_ms_per_frame": round(st.get("enqueue_ms", 0.0), 4),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
+                       "wide_tree": {"nodes_per_copy": info["wide_nodes"], "depth": info["wide_depth"]} if info["wide_nodes"] else None,
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
-                       "builder": "lbvh-gpu" if info["builder"] == 1 else (
-                           "sah-host" if os.environ.get("RT_SBVH", "") in ("0", "0.0") else "sbvh-host"),
+                       "builder": {0: "sah-host", 1: "lbvh-gpu", 2: "sbvh-host"}.get(info["builder"], str(info["builder"])),
                        "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
                                     "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),
                                     "upload": round(info["upload_ms"], 1)}, **more},

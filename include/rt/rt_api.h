@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 2
+#define RT_API_VERSION 3  /* 3: rt_stats.wave_node_bytes, RT_BUILDER_SBVH */
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -105,18 +105,26 @@ typedef struct rt_scene_opts {
                              * alone on the GPU is dispatched longest-first from an earlier frame's wave
                              * costs (small scenes also split their costliest waves); results never
                              * depend on the dispatch order */
-  int32_t builder;          /* RT_BUILDER_SAH (host SAH tree, default: fastest traversal; a spatial-split
-                             * BVH, or the plain binned-SAH tree with the environment variable RT_SBVH=0) or
-                             * RT_BUILDER_LBVH_GPU (Morton/radix-sort/Karras build on the
-                             * device in milliseconds; falls back to SAH when the tree would be too deep) */
+  int32_t builder;          /* the traversal tree's builder (results never depend on it):
+                             * RT_BUILDER_SBVH (rt_scene_opts_default: host SAH with spatial splits, the
+                             * fastest traversal; 1M faces ~4-5 s), RT_BUILDER_SAH (host binned SAH without
+                             * splits: ~4x faster build, ~5% slower traversal) or RT_BUILDER_LBVH_GPU
+                             * (Morton/radix-sort/Karras build on the device in milliseconds;
+                             * falls back to RT_BUILDER_SAH when the tree would be too deep) */
   int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_HOST (default,
                              * parallel passes on the host) or RT_BOXES_GPU (one launch per pass,
                              * one workgroup per box; identical boxes and face order; scenes with
                              * non-finite vertex coordinates use the host builder) */
+  int32_t wide_tree;        /* 1: also build the fp32 4-wide tree (eight per-octant copies of 128-B nodes in
+                             * HBM: ~8x the binary tree's node bytes) and walk it for PRIMARY packets whose
+                             * rays share a direction octant. 0 (default): the binary tree only -- measured
+                             * equal speed at a quarter of the memory. Results are
+                             * identical either way (API 3) */
 } rt_scene_opts;
 
 #define RT_BUILDER_SAH 0
 #define RT_BUILDER_LBVH_GPU 1
+#define RT_BUILDER_SBVH 2
 #define RT_BOXES_HOST 0
 #define RT_BOXES_GPU 1
 
@@ -144,6 +152,8 @@ typedef struct rt_scene_info {
   double bvh_gpu_ms;      /* device time of the LBVH kernels (RT_BUILDER_LBVH_GPU) */
   int32_t box_builder;    /* the box partition builder actually used (RT_BOXES_*) */
   double boxes_gpu_ms;    /* device time of the GPU box partition (RT_BOXES_GPU) */
+  int32_t wide_nodes;     /* fp32 4-wide nodes per octant copy (0: no wide tree) (API 3) */
+  int32_t wide_depth;     /* its depth */
 } rt_scene_info;
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);
@@ -252,6 +262,8 @@ typedef struct rt_stats {
   int64_t tri_tests;        /* RT_FRAME_STATS: sum over rays of triangle tests */
   int64_t wave_node_fetches;/* RT_FRAME_STATS: node records fetched (once per wave) */
   int64_t wave_tri_fetches; /* RT_FRAME_STATS: triangle records fetched (once per wave) */
+  int64_t wave_node_bytes;  /* RT_FRAME_STATS: bytes of the node records fetched (64 per binary record,
+                               128 per fp32 4-wide record; API 3) */
 } rt_stats;
 
 /* Renders the frame (this shard's tiles) on the scene's device and copies it into out_rgb
@@ -349,9 +361,10 @@ int rt_debug_math_host(int32_t op, int32_t n, const float* in, float* out);
 int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
 
 /* Host-side check of the scene's acceleration structures (tests only): every triangle lies inside
- * each ancestor box of the binary tree and of the 4-wide quantised tree, and every triangle record
- * sits in exactly one leaf of each. info[0..6] = binary nodes, binary depth, wide nodes, wide depth,
- * triangles reached (binary), triangles reached (wide), containment violations. RT_OK iff sound. */
+ * each ancestor box of the binary tree, of the 4-wide quantised tree and of the fp32 4-wide tree (whose
+ * per-octant child orders must be permutations), and every triangle record sits in exactly one leaf of
+ * each. info[0..6] = binary nodes, binary depth, quantised nodes, quantised depth, triangles reached
+ * (binary), triangles reached (quantised), violations (all three trees). RT_OK iff sound. */
 int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]);
 
 /* Kernel-variant override (tests and A/B measurements only; default 0 = the measured-best kernels):

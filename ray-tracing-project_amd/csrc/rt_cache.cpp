@@ -22,7 +22,7 @@ struct Header {
   int32_t nv, nf, n_mats, n_boxes, n_box_faces, n_nodes, n_nodes4, n_tris;
   uint32_t root;
   int32_t depth, leaves, depth4;
-  int32_t min_faces, max_boxes, leaf_size, pad;
+  int32_t min_faces, max_boxes, leaf_size, builder;  // builder: RT_BUILDER_* of the stored tree (was padding: 0)
   float M[16], Minv[16], MS[9], pad2[3];
 };
 
@@ -107,6 +107,7 @@ extern "C" int rt_scene_save(const rt_scene* s, const char* path) {
   h.min_faces = s->opts.min_faces;
   h.max_boxes = s->opts.max_boxes;
   h.leaf_size = s->opts.leaf_size;
+  h.builder = s->builder_used;
   memcpy(h.M, hs.M, sizeof h.M);
   memcpy(h.Minv, hs.Minv, sizeof h.Minv);
   memcpy(h.MS, hs.MS, sizeof h.MS);
@@ -160,7 +161,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
     return RT_ERR_IO;
   }
   if (h.nv < 0 || h.nf < 0 || h.n_mats < 0 || h.n_boxes < 0 || h.n_box_faces != h.nf || h.n_nodes < 0 ||
-      h.n_nodes4 < 0 || h.n_tris < h.nf || (int64_t)h.n_tris > 2 * (int64_t)h.nf + 1) {  // SBVH: references >= faces
+      h.n_nodes4 < 0 || h.n_tris < h.nf || (uint32_t)h.n_tris > rt::kMaxFaces) {  // SBVH: references >= faces
     rt::set_error("rt_scene_load: inconsistent header in %s", path);
     return RT_ERR_IO;
   }
@@ -170,6 +171,9 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
   s->opts.min_faces = h.min_faces;
   s->opts.max_boxes = h.max_boxes;
   s->opts.leaf_size = h.leaf_size;
+  if (h.builder < RT_BUILDER_SAH || h.builder > RT_BUILDER_SBVH) { rt::set_error("rt_scene_load: bad builder id in %s", path); return RT_ERR_IO; }
+  s->opts.builder = h.builder;
+  s->builder_used = h.builder;
   s->opts.frames_in_flight = std::max(1, std::min(s->opts.frames_in_flight, (int32_t)rt_scene::kMaxSlots));
   rt::HostScene& hs = s->hs;
   hs.nv = h.nv;
@@ -236,7 +240,8 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
   for (const rt::Node4Q& n : hs.nodes4)
     for (int c = 0; c < 4; c++)
       if (((n.valid >> c) & 1) && !handle_ok(n.child[c], h.n_nodes4)) { rt::set_error("rt_scene_load: bad wide BVH"); return RT_ERR_IO; }
-  if (h.nf > 0 && !handle_ok(h.root, h.n_nodes)) { rt::set_error("rt_scene_load: bad BVH root"); return RT_ERR_IO; }
+  // the root, whenever there are nodes (also for a face-less file: the tree walk below starts there)
+  if ((h.nf > 0 || h.n_nodes > 0) && !handle_ok(h.root, h.n_nodes)) { rt::set_error("rt_scene_load: bad BVH root"); return RT_ERR_IO; }
   // Shape checks (the content hash is not a signature: a crafted file can carry a valid one). Each
   // tree must be a tree: walked from its root, every interior node is reached exactly once (no
   // cycle, no shared subtree), and its depth is recomputed here, never taken from the header, then
@@ -289,6 +294,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
       hs.depth4 = hs.nodes4.empty() ? 0 : maxd + 1;
     }
   }
+  if (s->opts.wide_tree) rt::build_wide(hs);  // derived from the validated binary tree (not stored)
   s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (s->opts.device != RT_DEVICE_NONE) {
     const int rc = rt::device_upload(s.get());

@@ -150,7 +150,8 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 // ST_WPOP / ST_WCULL (counting run, closest hit): stack pops per wave, and those pops at which no lane
 // that wanted the entry still could (every such lane's entry distance into it, recorded at the push,
 // now beyond its closest hit) -- what culling at the pop would save (rt_debug_counters)
-enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_COUNT };
+// ST_WWIDE: 128-B fp32 4-wide node records fetched per wave (ST_WNODE: 64-B binary / quantised records)
+enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_WWIDE, ST_COUNT };
 constexpr int kStatSlots = 16;
 
 struct Hit {
@@ -161,16 +162,45 @@ struct Hit {
 
 struct Ray {
   f3 o, d;      // world space (triangle tests)
-  f3 id, oid;   // culling: 1/d (zeros nudged), -o/d
+  f3 id;        // culling: 1/d (zeros nudged)
+  f3 oa, ob;    // culling: -(o + p)/d and -(o - p)/d, the lo / hi plane offsets of boxes grown by p
   f3 o2, d2;    // object space (reference intersectBox): Minv*o_box, normalized(MS*d)
 };
 
 __device__ __forceinline__ float nudge(float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; }
 
+// Culling set-up of a ray, once per ray.
+// The BVH boxes carry a static pad for the scene-scale rounding of the reference's arithmetic (bvh_pad,
+// rt_host.cpp). The rounding of the reference's hit point P = o + t d, and of this slab test, also grows
+// with the ray origin's magnitude: both are a few ulp of |o| + |t d| <= 2|o| + R per axis (R: the scene's
+// magnitude). So every ray grows the boxes it tests by its own pad p = kCullPadRel * |o|_inf, folded into
+// two per-axis offsets: with box [lo - p, hi + p] the plane distances are fma(lo, 1/d, -(o + p)/d) and
+// fma(hi, 1/d, -(o - p)/d). That costs no instruction per node (the octant loops pick the offset of each
+// plane at compile time). kCullPadRel = 4e-5 is ~100x the worst-case rounding (<= 6 ulp of |o|, each
+// 2^-24 |o|), so for every origin the culling never drops a face the reference accepts.
+// Outside the range where these products stay finite (|o|_inf > 1e18, |d|_inf outside [1e-12, 1e18], or
+// non-finite input) the ray's boxes grow without bound instead: p = inf, every box is entered, and the
+// packet tests every triangle with the exact test -- still the reference's result, by brute force.
+#ifndef RT_DYN_PAD  // 0: static pad only (round-2 behaviour, kept to demonstrate the far-origin tests failing)
+#define RT_DYN_PAD 1
+#endif
+constexpr float kCullPadRel = 4e-5f, kCullOriginMax = 1e18f, kCullDirMin = 1e-12f, kCullDirMax = 1e18f;
 __device__ __forceinline__ void setup_cull(Ray& r) {
-  r.id = f3{__builtin_amdgcn_rcpf(nudge(r.d.x)), __builtin_amdgcn_rcpf(nudge(r.d.y)),
-            __builtin_amdgcn_rcpf(nudge(r.d.z))};
-  r.oid = f3{-r.o.x * r.id.x, -r.o.y * r.id.y, -r.o.z * r.id.z};
+  const float om = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
+  const float dm = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+  const bool certified = !RT_DYN_PAD || (om <= kCullOriginMax && dm >= kCullDirMin && dm <= kCullDirMax);  // false for NaN
+  if (certified) {
+    r.id = f3{__builtin_amdgcn_rcpf(nudge(r.d.x)), __builtin_amdgcn_rcpf(nudge(r.d.y)),
+              __builtin_amdgcn_rcpf(nudge(r.d.z))};
+    const float p = RT_DYN_PAD ? kCullPadRel * om : 0.0f;
+    r.oa = f3{-(r.o.x + p) * r.id.x, -(r.o.y + p) * r.id.y, -(r.o.z + p) * r.id.z};
+    r.ob = f3{-(r.o.x - p) * r.id.x, -(r.o.y - p) * r.id.y, -(r.o.z - p) * r.id.z};
+  } else {
+    // unbounded boxes: lo planes at -inf, hi planes at +inf along the (kept) direction signs
+    r.id = f3{copysignf(1.0f, nudge(r.d.x)), copysignf(1.0f, nudge(r.d.y)), copysignf(1.0f, nudge(r.d.z))};
+    r.oa = f3{-r.id.x * INFINITY, -r.id.y * INFINITY, -r.id.z * INFINITY};
+    r.ob = f3{r.id.x * INFINITY, r.id.y * INFINITY, r.id.z * INFINITY};
+  }
 }
 
 #ifndef RT_TRI_VREG  // edge differences from VGPR copies of w0 / w1 (fewer moves)
@@ -179,9 +209,6 @@ __device__ __forceinline__ void setup_cull(Ray& r) {
 #ifndef RT_EYE_VREG  // k_primary_fused keeps the eye in VGPRs
 #define RT_EYE_VREG 1
 #endif
-#ifndef RT_PK_SLAB  // octant slabs as v_pk_fma_f32 over the (lo, hi) coordinate pairs
-#define RT_PK_SLAB 0
-#endif
 // Conservative slab test for one padded child box (culling only; exactness comes from padding):
 // returns the entry distance tmin and the exit distance clipped to [0, tmax_ray] (hit iff tmin <= tmax)
 struct Span {
@@ -189,16 +216,16 @@ struct Span {
 };
 __device__ __forceinline__ Span slab(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
                                      float tmax_ray) {
-  const float tx0 = __builtin_fmaf(lx, r.id.x, r.oid.x), tx1 = __builtin_fmaf(hx, r.id.x, r.oid.x);
-  const float ty0 = __builtin_fmaf(ly, r.id.y, r.oid.y), ty1 = __builtin_fmaf(hy, r.id.y, r.oid.y);
-  const float tz0 = __builtin_fmaf(lz, r.id.z, r.oid.z), tz1 = __builtin_fmaf(hz, r.id.z, r.oid.z);
+  const float tx0 = __builtin_fmaf(lx, r.id.x, r.oa.x), tx1 = __builtin_fmaf(hx, r.id.x, r.ob.x);
+  const float ty0 = __builtin_fmaf(ly, r.id.y, r.oa.y), ty1 = __builtin_fmaf(hy, r.id.y, r.ob.y);
+  const float tz0 = __builtin_fmaf(lz, r.id.z, r.oa.z), tz1 = __builtin_fmaf(hz, r.id.z, r.ob.z);
   Span s;
   s.tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
   s.tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_ray));
   return s;
 }
 // The same span when the wave's active rays share one direction octant (OCT bit k: axis k negative,
-// by the sign of the nudged reciprocal): fma(., id, oid) is monotone in the box coordinate, so the
+// by the sign of the nudged reciprocal): fma(., id, offset) is monotone in the box coordinate, so the
 // near / far plane of each axis is known and min(t0, t1) / max(t0, t1) are exactly the near / far
 // values -- identical results with 8 fewer min/max per child. OCT < 0: the generic test.
 #ifndef RT_CLIP_ASM
@@ -208,46 +235,26 @@ template <int OCT>
 __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
                                        float tmax_ray) {
   if (OCT < 0) return slab(lx, hx, ly, hy, lz, hz, r, tmax_ray);
-#if RT_PK_SLAB
-  {
-    // both planes of an axis in one packed fma: the record's (lo, hi) pair is an aligned SGPR pair, the
-    // ray's id / oid are held pairwise as (id.x, id.y), (id.z, oid.x), (oid.y, oid.z) and broadcast by
-    // op_sel (each half rounded once, as v_fma_f32)
-    auto pk = [](float a, float b) { return ((uint64_t)__float_as_uint(b) << 32) | __float_as_uint(a); };
-    const uint64_t pa = pk(r.id.x, r.id.y), pb = pk(r.id.z, r.oid.x), pc = pk(r.oid.y, r.oid.z);
-    uint64_t tx, ty, tz;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tx) : "s"(pk(lx, hx)), "v"(pa), "v"(pb));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(ty) : "s"(pk(ly, hy)), "v"(pa), "v"(pc));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tz) : "s"(pk(lz, hz)), "v"(pb), "v"(pc));
-    const float tx0 = __uint_as_float((uint32_t)tx), tx1 = __uint_as_float((uint32_t)(tx >> 32));
-    const float ty0 = __uint_as_float((uint32_t)ty), ty1 = __uint_as_float((uint32_t)(ty >> 32));
-    const float tz0 = __uint_as_float((uint32_t)tz), tz1 = __uint_as_float((uint32_t)(tz >> 32));
-    const float nx = (OCT & 1) ? tx1 : tx0, fx = (OCT & 1) ? tx0 : tx1;
-    const float ny = (OCT & 2) ? ty1 : ty0, fy = (OCT & 2) ? ty0 : ty1;
-    const float nz = (OCT & 4) ? tz1 : tz0, fz = (OCT & 4) ? tz0 : tz1;
-    Span s;
-    // (as asm: the compiler would canonicalise the asm-produced planes with an extra v_max each)
-    asm("v_max_f32 %0, 0, %3\n\tv_max3_f32 %0, %1, %2, %0" : "=&v"(s.tmin) : "v"(nx), "v"(ny), "v"(nz));
-    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(s.tmax) : "v"(fx), "v"(fy), "v"(fz), "v"(tmax_ray));
-    return s;
-  }
-#endif
+  // near plane of a positive axis: lo (offset oa); of a negative axis: hi (offset ob); far the other
   const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
   const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
   const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
+  const float nox = (OCT & 1) ? r.ob.x : r.oa.x, fox = (OCT & 1) ? r.oa.x : r.ob.x;
+  const float noy = (OCT & 2) ? r.ob.y : r.oa.y, foy = (OCT & 2) ? r.oa.y : r.ob.y;
+  const float noz = (OCT & 4) ? r.ob.z : r.oa.z, foz = (OCT & 4) ? r.oa.z : r.ob.z;
   Span s;
-  s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, r.oid.x), __builtin_fmaf(ny, r.id.y, r.oid.y)),
-                 fmaxf(__builtin_fmaf(nz, r.id.z, r.oid.z), 0.0f));
+  s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
+                 fmaxf(__builtin_fmaf(nz, r.id.z, noz), 0.0f));
 #if RT_CLIP_ASM
   // min of the three far planes and tmax_ray in two instructions (the compiler's fminf would first
   // canonicalise tmax_ray, a loop-carried value, with an extra v_max per node)
   asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
       : "=&v"(s.tmax)
-      : "v"(__builtin_fmaf(fx, r.id.x, r.oid.x)), "v"(__builtin_fmaf(fy, r.id.y, r.oid.y)),
-        "v"(__builtin_fmaf(fz, r.id.z, r.oid.z)), "v"(tmax_ray));
+      : "v"(__builtin_fmaf(fx, r.id.x, fox)), "v"(__builtin_fmaf(fy, r.id.y, foy)),
+        "v"(__builtin_fmaf(fz, r.id.z, foz)), "v"(tmax_ray));
 #else
-  s.tmax = fminf(fminf(__builtin_fmaf(fx, r.id.x, r.oid.x), __builtin_fmaf(fy, r.id.y, r.oid.y)),
-                 fminf(__builtin_fmaf(fz, r.id.z, r.oid.z), tmax_ray));
+  s.tmax = fminf(fminf(__builtin_fmaf(fx, r.id.x, fox), __builtin_fmaf(fy, r.id.y, foy)),
+                 fminf(__builtin_fmaf(fz, r.id.z, foz), tmax_ray));
 #endif
   return s;
 }
@@ -447,7 +454,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       {
         Ray r2 = r;
         float tc2 = tcut;
-        asm volatile("" : "+v"(r2.id.x), "+v"(r2.id.y), "+v"(r2.id.z), "+v"(r2.oid.x), "+v"(r2.oid.y), "+v"(r2.oid.z), "+v"(tc2));
+        asm volatile("" : "+v"(r2.id.x), "+v"(r2.id.y), "+v"(r2.id.z), "+v"(r2.oa.x), "+v"(r2.oa.y), "+v"(r2.oa.z), "+v"(tc2));
         const Span q0 = slab(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r2, tc2);
         const Span q1 = slab(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r2, tc2);
         uint64_t mm = mask_le(q0.tmin, q0.tmax) | mask_le(q1.tmin, q1.tmax);
@@ -820,6 +827,260 @@ __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, b
 }
 
 // ------------------------------------------------------------------------------------------------
+// fp32 4-wide packet traversal (Node128, the default PRIMARY tree). A node step fetches the 128-B record
+// with two s_load_dwordx16 under one wait, slab-tests the four children per lane (exact fp32 boxes, no
+// dequantisation), and -- the children being stored in this octant's near-to-far order -- writes every
+// hit child to the wave stack farthest first with a conditional increment, takes the nearest hit child
+// as the next node and drops it from the top again: no sort, no lane vote, 14 SALU. Same exact triangle
+// tests and (t, rank) argmin as the binary loops, so every result is identical; only the visit order
+// differs. Half the dependent node fetches of the binary tree per wave (SBVH soup: 52 vs 100 per wave).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ Node128 sload128(const void* base, uint32_t off) {
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t o = __builtin_amdgcn_readfirstlane(off);
+  i16v lo, hi;
+  asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %3 offset:0x40\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(lo), "=&s"(hi)
+               : "s"(bs), "s"(o)
+               : "memory");
+  Node128 r;
+  __builtin_memcpy(&r, &lo, 64);
+  __builtin_memcpy(reinterpret_cast<char*>(&r) + 64, &hi, 64);
+  return r;
+}
+
+// Reference form with the counting run's statistics (RT_FRAME_STATS): the same visit order as
+// traverse_wide_fast. OCT < 0 (mixed-octant packets): the generic slab test, copy 0's child order.
+template <bool ANY, bool STATS, int OCT>
+__device__ __forceinline__ void traverse_wide(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                              uint32_t* lds_stack, uint64_t* lds_mask, uint32_t* cnt) {
+  uint64_t act = ballot(active);
+  float tlim = active ? INFINITY : -1.0f;
+  if (!ANY && !active) h.t = -1.0f;
+  bool want = active;
+  int sp = 0;
+  uint32_t node = P.wide_base + (uint32_t)(OCT < 0 ? 0 : OCT) * P.wide_copy_bytes;
+  for (;;) {
+    while (!is_leaf(node)) {
+      const Node128 nd = sload128(P.nodes, node);
+      if (STATS) {
+        if (want) cnt[ST_NODE]++;
+        cnt[ST_WWIDE]++;
+      }
+      const float tcut = ANY ? tlim : h.t;
+      uint64_t m[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float* b = nd.box[c];
+        const Span s = slab_o<OCT>(b[0], b[1], b[2], b[3], b[4], b[5], r, tcut);
+        m[c] = mask_le(s.tmin, s.tmax);
+      }
+      uint32_t nxt = kPopMarker;
+      uint64_t wm = 0;
+#pragma unroll
+      for (int c = 3; c >= 0; c--) {  // farthest first; the nearest hit ends on top and is taken next
+        lds_stack[sp] = nd.child[c];
+        if (STATS) lds_mask[sp] = m[c];
+        if (m[c] != 0) {
+          nxt = nd.child[c];
+          wm = m[c];
+          sp++;
+        }
+      }
+      sp = (int)uniform((uint32_t)sp);
+      if (nxt != kPopMarker) sp--;
+      if (STATS) want = (wm >> lane_id()) & 1;
+      node = uniform(nxt);
+    }
+    if (node != kPopMarker) {
+      const uint32_t first = leaf_first(node), count = leaf_count(node);
+      if (STATS) {
+        if (want) cnt[ST_TRI] += count;
+        cnt[ST_WTRI] += count;
+      }
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = sload_tri(P.tris, first + k);
+        test_tri<ANY>(P, tr, first + k, r, act, h, found);
+      }
+      if (ANY) {
+        active = active & !found;
+        act = ballot(active);
+        if (!act) break;
+        tlim = active ? INFINITY : -1.0f;
+      }
+    }
+    if (sp == 0) break;
+    sp--;
+    node = uniform(lds_stack[sp]);
+    if (STATS) {
+      want = (lds_mask[sp] >> lane_id()) & 1;
+      cnt[ST_WPOP]++;
+    }
+  }
+  if (!ANY && !active) h.t = INFINITY;
+}
+
+// RT_WIDE_PF: scalar-cache prefetch per wide node step (default 4, measured best: profiles/ab/r03_wide_tree_ab.txt) -- 2: both 64-B halves of every child's record
+// (8 one-dword loads), 1: the first half of every child's, 3: both halves of the two nearest children,
+// 4: both halves of the nearest child, 0: none
+#ifndef RT_WIDE_PF
+#define RT_WIDE_PF 4
+#endif
+// The production form (octant loops, no counting): node fetch + child prefetches, the four slab tests,
+// and the decision as one SALU block interleaved with the four stack writes.
+template <bool ANY, int OCT>
+__device__ __forceinline__ void traverse_wide_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
+                                                   uint32_t* lds_stack) {
+  uint64_t act = ballot(active);
+  float tlim = active ? INFINITY : -1.0f;
+  if (!ANY && !active) h.t = -1.0f;
+  int sp = 0;
+  const uint32_t vbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)lds_stack;
+  const uint64_t bb = (uint64_t)P.nodes;
+  const uint64_t bs = ((uint64_t)uniform((uint32_t)(bb >> 32)) << 32) | (uint32_t)uniform((uint32_t)bb);
+  uint32_t sink = 0;  // the prefetches' destination (values unused): retired by the next node load's wait
+  // RT_WIDE_PF 5 / 6: vector prefetches into L2 (their own counter, vmcnt: no scalar wait is tied to
+  // them; retired once at the end). Lane l loads half l & 1 of child `first + min(l >> 1, 3 - first)`.
+  uint32_t vsink = 0;
+  const int vlane = (int)(threadIdx.x & 63);
+  const int vfirst = RT_WIDE_PF == 5 ? 1 : 0;
+  const int vsel = min(vfirst + (vlane >> 1), 3);
+  const uint32_t vhalf = (uint32_t)(vlane & 1) * 64u;
+  uint32_t node = uniform(P.wide_base + (uint32_t)OCT * P.wide_copy_bytes);
+  Ray rr = r;
+  // the node loop is rotated: the record load that follows a descent sits at the end of the loop body
+  // and a separate copy serves the entry after a pop, so a wait the compiler needs after the leaf path
+  // (its kernel-argument reloads) stays on that path instead of heading every node step
+  auto load = [&](uint32_t off, i16v& lo, i16v& hi) {
+    asm volatile("s_load_dwordx16 %0, %3, %4\n\ts_load_dwordx16 %1, %3, %4 offset:0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(lo), "=&s"(hi), "+&s"(sink)
+                 : "s"(bs), "s"(off)
+                 : "memory");
+  };
+  for (;;) {
+    if (!is_leaf(node)) {
+      i16v lo, hi;
+      load(node, lo, hi);
+      for (;;) {
+      Node128 nd;
+      __builtin_memcpy(&nd, &lo, 64);
+      __builtin_memcpy(reinterpret_cast<char*>(&nd) + 64, &hi, 64);
+      // the ray's reciprocal direction passes through the prefetch asm ("+v", carried across steps: no
+      // copies), so the slab tests that read it cannot be scheduled above the prefetches: those are issued
+      // the moment the node has arrived
+      if (RT_WIDE_PF == 2) {
+        asm volatile("s_load_dword %[k], %[b], %[p0]\n\ts_load_dword %[k], %[b], %[p0] offset:0x40\n\t"
+                     "s_load_dword %[k], %[b], %[p1]\n\ts_load_dword %[k], %[b], %[p1] offset:0x40\n\t"
+                     "s_load_dword %[k], %[b], %[p2]\n\ts_load_dword %[k], %[b], %[p2] offset:0x40\n\t"
+                     "s_load_dword %[k], %[b], %[p3]\n\ts_load_dword %[k], %[b], %[p3] offset:0x40"
+                     : [k] "+&s"(sink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
+                     : [b] "s"(bs), [p0] "s"(uniform(nd.pf[0])), [p1] "s"(uniform(nd.pf[1])), [p2] "s"(uniform(nd.pf[2])),
+                       [p3] "s"(uniform(nd.pf[3]))
+                     : "memory");
+      } else if (RT_WIDE_PF == 3) {  // both halves of the two nearest children only
+        asm volatile("s_load_dword %[k], %[b], %[p0]\n\ts_load_dword %[k], %[b], %[p0] offset:0x40\n\t"
+                     "s_load_dword %[k], %[b], %[p1]\n\ts_load_dword %[k], %[b], %[p1] offset:0x40"
+                     : [k] "+&s"(sink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
+                     : [b] "s"(bs), [p0] "s"(uniform(nd.pf[0])), [p1] "s"(uniform(nd.pf[1]))
+                     : "memory");
+      } else if (RT_WIDE_PF == 4) {  // both halves of the nearest child only
+        asm volatile("s_load_dword %[k], %[b], %[p0]\n\ts_load_dword %[k], %[b], %[p0] offset:0x40"
+                     : [k] "+&s"(sink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
+                     : [b] "s"(bs), [p0] "s"(uniform(nd.pf[0]))
+                     : "memory");
+      } else if (RT_WIDE_PF == 1) {
+        asm volatile("s_load_dword %[k], %[b], %[p0]\n\ts_load_dword %[k], %[b], %[p1]\n\t"
+                     "s_load_dword %[k], %[b], %[p2]\n\ts_load_dword %[k], %[b], %[p3]"
+                     : [k] "+&s"(sink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
+                     : [b] "s"(bs), [p0] "s"(uniform(nd.pf[0])), [p1] "s"(uniform(nd.pf[1])), [p2] "s"(uniform(nd.pf[2])),
+                       [p3] "s"(uniform(nd.pf[3]))
+                     : "memory");
+      } else if (RT_WIDE_PF == 5 || RT_WIDE_PF == 6) {
+        // 5: the nearest child into the scalar cache (both halves), the other three into L2 by one vector
+        // load; 6: all four into L2 by one vector load
+        if (RT_WIDE_PF == 5)
+          asm volatile("s_load_dword %[k], %[b], %[p0]\n\ts_load_dword %[k], %[b], %[p0] offset:0x40"
+                       : [k] "+&s"(sink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
+                       : [b] "s"(bs), [p0] "s"(uniform(nd.pf[0]))
+                       : "memory");
+        const uint32_t p1 = uniform(nd.pf[1]), p2 = uniform(nd.pf[2]), p3 = uniform(nd.pf[3]);
+        const uint32_t po = (vsel == 0 ? uniform(nd.pf[0]) : vsel == 1 ? p1 : vsel == 2 ? p2 : p3) + vhalf;
+        asm volatile("global_load_dword %[k], %[o], %[b]"
+                     : [k] "+&v"(vsink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
+                     : [o] "v"(po), [b] "s"(bs)
+                     : "memory");
+      }
+      // the handles into VGPRs for the stack writes (off the masks' critical path)
+      uint32_t v0 = nd.child[0], v1 = nd.child[1], v2 = nd.child[2], v3 = nd.child[3];
+      asm("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+      const float tcut = ANY ? tlim : h.t;
+      uint64_t m[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float* b = nd.box[c];
+        const Span s = slab_o<OCT>(b[0], b[1], b[2], b[3], b[4], b[5], rr, tcut);
+        m[c] = mask_le(s.tmin, s.tmax);
+      }
+      sp = (int)uniform((uint32_t)sp);
+      uint32_t nxt, a0, a1, a2, a3;
+      asm volatile(
+          "v_lshl_add_u32 %[a3], %[sp], 2, %[vb]\n\t"
+          "s_cmp_lg_u64 %[m3], 0\n\t"
+          "s_cselect_b32 %[nxt], %[h3], -1\n\t"
+          "s_addc_u32 %[sp], %[sp], 0\n\t"
+          "ds_write_b32 %[a3], %[v3]\n\t"
+          "v_lshl_add_u32 %[a2], %[sp], 2, %[vb]\n\t"
+          "s_cmp_lg_u64 %[m2], 0\n\t"
+          "s_cselect_b32 %[nxt], %[h2], %[nxt]\n\t"
+          "s_addc_u32 %[sp], %[sp], 0\n\t"
+          "ds_write_b32 %[a2], %[v2]\n\t"
+          "v_lshl_add_u32 %[a1], %[sp], 2, %[vb]\n\t"
+          "s_cmp_lg_u64 %[m1], 0\n\t"
+          "s_cselect_b32 %[nxt], %[h1], %[nxt]\n\t"
+          "s_addc_u32 %[sp], %[sp], 0\n\t"
+          "ds_write_b32 %[a1], %[v1]\n\t"
+          "v_lshl_add_u32 %[a0], %[sp], 2, %[vb]\n\t"
+          "s_cmp_lg_u64 %[m0], 0\n\t"
+          "s_cselect_b32 %[nxt], %[h0], %[nxt]\n\t"
+          "s_addc_u32 %[sp], %[sp], 0\n\t"
+          "ds_write_b32 %[a0], %[v0]\n\t"
+          "s_cmp_lg_u32 %[nxt], -1\n\t"
+          "s_subb_u32 %[sp], %[sp], 0"
+          : [nxt] "=&s"(nxt), [sp] "+&s"(sp), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3)
+          : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3]), [h0] "s"(uniform(nd.child[0])),
+            [h1] "s"(uniform(nd.child[1])), [h2] "s"(uniform(nd.child[2])), [h3] "s"(uniform(nd.child[3])),
+            [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3), [vb] "v"(vbase)
+          : "scc", "memory");
+      node = nxt;
+      if (is_leaf(node)) break;
+      load(node, lo, hi);
+      }
+    }
+    if (node != kPopMarker) {
+      const uint32_t first = leaf_first(node), count = leaf_count(node);
+      for (uint32_t k = 0; k < count; k++) {
+        const TriRec64 tr = sload_tri(P.tris, first + k);
+        test_tri<ANY>(P, tr, first + k, r, act, h, found);
+      }
+      if (ANY) {
+        active = active & !found;
+        act = ballot(active);
+        if (!act) break;
+        tlim = active ? INFINITY : -1.0f;
+      }
+    }
+    if (sp == 0) break;
+    sp--;
+    node = uniform(lds_stack[sp]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(sink) : "memory");  // the last prefetches have landed
+  if (RT_WIDE_PF == 5 || RT_WIDE_PF == 6) asm volatile("s_waitcnt vmcnt(0)" ::"v"(vsink) : "memory");
+  if (!ANY && !active) h.t = INFINITY;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Dual-chain traversal (PRIMARY, closest hit): one wave walks the BVH for TWO independent 8x8 packets
 // at once -- two node handles, two LDS stacks, two rays per lane. Each node step fetches both packets'
 // records with one wait and then runs both box tests and decisions, so the two dependent fetch ->
@@ -1005,19 +1266,19 @@ __device__ __forceinline__ void traverse4(const DevScene& P, const Ray& r, bool 
       const float sx = __uint_as_float((uint32_t)nd.ex << 23) * r.id.x;
       const float sy = __uint_as_float((uint32_t)nd.ey << 23) * r.id.y;
       const float sz = __uint_as_float((uint32_t)nd.ez << 23) * r.id.z;
-      const float bx = __builtin_fmaf(nd.ox, r.id.x, r.oid.x);
-      const float by = __builtin_fmaf(nd.oy, r.id.y, r.oid.y);
-      const float bz = __builtin_fmaf(nd.oz, r.id.z, r.oid.z);
+      const float bx = __builtin_fmaf(nd.ox, r.id.x, r.oa.x), bxh = __builtin_fmaf(nd.ox, r.id.x, r.ob.x);
+      const float by = __builtin_fmaf(nd.oy, r.id.y, r.oa.y), byh = __builtin_fmaf(nd.oy, r.id.y, r.ob.y);
+      const float bz = __builtin_fmaf(nd.oz, r.id.z, r.oa.z), bzh = __builtin_fmaf(nd.oz, r.id.z, r.ob.z);
       uint64_t m[4];
       float tm[4];
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         const float tx0 = __builtin_fmaf((float)((nd.qlx >> (8 * c)) & 255u), sx, bx);
-        const float tx1 = __builtin_fmaf((float)((nd.qhx >> (8 * c)) & 255u), sx, bx);
+        const float tx1 = __builtin_fmaf((float)((nd.qhx >> (8 * c)) & 255u), sx, bxh);
         const float ty0 = __builtin_fmaf((float)((nd.qly >> (8 * c)) & 255u), sy, by);
-        const float ty1 = __builtin_fmaf((float)((nd.qhy >> (8 * c)) & 255u), sy, by);
+        const float ty1 = __builtin_fmaf((float)((nd.qhy >> (8 * c)) & 255u), sy, byh);
         const float tz0 = __builtin_fmaf((float)((nd.qlz >> (8 * c)) & 255u), sz, bz);
-        const float tz1 = __builtin_fmaf((float)((nd.qhz >> (8 * c)) & 255u), sz, bz);
+        const float tz1 = __builtin_fmaf((float)((nd.qhz >> (8 * c)) & 255u), sz, bzh);
         const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
         const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcut));
         m[c] = mask_le(tmin, tmax) & act & bitmask64(nd.valid, c);
@@ -1197,9 +1458,10 @@ enum { TRAV_B2_VGPR = 0, TRAV_B2_LDS = 1, TRAV_W4 = 2, TRAV_LANE = 3 };
 
 template <int TRAV, bool STATS>
 struct WaveLds {
-  static constexpr int kEntries = TRAV == TRAV_W4 ? kStack4 : (TRAV == TRAV_LANE ? 1 : 64);
+  // binary LDS-stack kernels also run the fp32 4-wide loops (traverse_wide*): kStackW entries
+  static constexpr int kEntries = TRAV == TRAV_W4 ? kStack4 : (TRAV == TRAV_LANE ? 1 : (TRAV == TRAV_B2_LDS ? kStackW : 64));
   uint32_t stack[4][kEntries];
-  uint64_t mask[4][(STATS && TRAV == TRAV_W4) ? kEntries : 1];
+  uint64_t mask[4][(STATS && (TRAV == TRAV_W4 || TRAV == TRAV_B2_LDS)) ? kEntries : 1];
   uint32_t clk[4];  // one-wave kernels: the wave's start clocks (wave_clock_start), kept out of registers
 };
 
@@ -1217,7 +1479,9 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
 #ifndef RT_OCT_SPECIALIZE
 #define RT_OCT_SPECIALIZE 1
 #endif
-template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false>
+// WIDE: packets whose rays share an octant walk the fp32 4-wide tree when the scene has one
+// (traverse_wide_fast; the counting run traverse_wide); mixed-octant packets keep the binary loop.
+template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false, bool WIDE = false>
 __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                           WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   if (RT_OCT_SPECIALIZE && (TRAV == TRAV_B2_LDS || TRAV == TRAV_B2_VGPR)) {
@@ -1227,6 +1491,20 @@ __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool 
                    sz = ballot(__float_as_uint(r.id.z) >> 31) & act;
     if ((sx == 0 || sx == act) && (sy == 0 || sy == act) && (sz == 0 || sz == act)) {
       const int oct = (sx ? 1 : 0) | (sy ? 2 : 0) | (sz ? 4 : 0);
+      if (WIDE && SL && P.wide_copy_bytes != 0) {
+        uint32_t* st = L.stack[wv];
+        uint64_t* mk = L.mask[STATS ? wv : 0];
+#define RT_WIDE_CASE(o)                                                              \
+  case o:                                                                           \
+    if (STATS) traverse_wide<ANY, STATS, o>(P, r, active, h, found, st, mk, cnt);   \
+    else traverse_wide_fast<ANY, o>(P, r, active, h, found, st);                    \
+    return;
+        switch (oct) {
+          RT_WIDE_CASE(0) RT_WIDE_CASE(1) RT_WIDE_CASE(2) RT_WIDE_CASE(3)
+          RT_WIDE_CASE(4) RT_WIDE_CASE(5) RT_WIDE_CASE(6) default: RT_WIDE_CASE(7)
+        }
+#undef RT_WIDE_CASE
+      }
       if (RT_FAST_LOOP && !STATS && SL) {
         switch (oct) {
           case 0: traverse_fast<ANY, 0>(P, r, active, h, found, L.stack[wv]); return;
@@ -1258,11 +1536,11 @@ __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool 
   }
   trace<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
 }
-template <bool STATS, int TRAV>
+template <bool STATS, int TRAV, bool WIDE = false>
 __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& r, bool active, Hit& h,
                                                   WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   bool found = false;
-  trace_oct<false, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
+  trace_oct<false, STATS, TRAV, false, WIDE>(P, r, active, h, found, L, wv, cnt);
 }
 
 // FULL mode: primary, reflection and shadow packets also take the octant-specialised loops when the
@@ -1555,7 +1833,7 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
 #pragma unroll
   for (int c = 0; c < ST_COUNT; c++) {
     unsigned long long v = cnt[c];
-    if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL) v = (lane == 0) ? v : 0;  // wave counts once
+    if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL || c == ST_WWIDE) v = (lane == 0) ? v : 0;  // wave counts once
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(P.stats + c, v);
   }
@@ -1646,7 +1924,7 @@ void k_trace_primary(FrameParams P) {
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && c.active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  trace_closest_oct<STATS, TRAV>(P.sc, r, c.active, h, lds, c.slot, cnt);
+  trace_closest_oct<STATS, TRAV, true>(P.sc, r, c.active, h, lds, c.slot, cnt);
   if (STATS && c.active && h.t != INFINITY) cnt[ST_HITS]++;
   if (c.active) P.hits[(size_t)c.py * P.W + c.px] = make_uint2(__float_as_uint(h.t), h.slot);
   if (P.wcount0 != nullptr) {  // FULL pipeline: per-wave hit count for the list0 compaction
@@ -1879,7 +2157,7 @@ void k_primary_fused(FrameParams P) {
   const Ray r = primary_ray(P, c.px, c.py);
 #endif
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
+  trace_closest_oct<false, TRAV_B2_LDS, true>(P.sc, r, c.active, h, lds, c.slot, nullptr);
   if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
   wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
 }
@@ -2649,10 +2927,21 @@ int device_upload(rt_scene* s) {
     // base plus a 32-bit byte offset reaches either: with RT_PREFETCH each uploaded node's pad0 / pad1
     // hold the offsets of its children's records (a leaf child: its first triangle)
     const size_t nn = hs.nodes.size(), nt = hs.tris.size();
-    const size_t bytes = (nn + nt) * 64;
+    size_t bytes = (nn + nt) * 64;
     if (bytes > 0xFFFFFFFFull) {  // cannot happen below kMaxFaces (rt_scene_create checks it)
       set_error("scene records exceed 4 GiB (%zu nodes, %zu triangles)", nn, nt);
       return RT_ERR_INVALID;
+    }
+    // the fp32 4-wide tree's eight octant copies follow, 128-B aligned (one L2 line per record), when
+    // the whole allocation stays addressable by 32-bit byte offsets; else the binary tree serves alone
+    const size_t nw = hs.wide.size(), wide_base = (bytes + 127) & ~(size_t)127;
+    const size_t wide_bytes = 8 * nw * sizeof(Node128);
+    s->wide_base = 0;
+    s->wide_copy_bytes = 0;
+    if (nw > 0 && wide_base + wide_bytes <= 0xFFFFFFFFull) {
+      s->wide_base = (uint32_t)wide_base;
+      s->wide_copy_bytes = (uint32_t)(nw * sizeof(Node128));
+      bytes = wide_base + wide_bytes;
     }
     if ((rc = dalloc_copy(&s->d_nodes, nullptr, bytes, tot))) return rc;
     std::vector<Node64> nodes(hs.nodes);
@@ -2675,6 +2964,33 @@ int device_upload(rt_scene* s) {
     if (nn) HIPCHECK(hipMemcpy(s->d_nodes, nodes.data(), nn * 64, hipMemcpyHostToDevice));
     s->d_tris = reinterpret_cast<TriRec64*>(s->d_nodes + nn);
     if (nt) HIPCHECK(hipMemcpy(s->d_tris, hs.tris.data(), nt * 64, hipMemcpyHostToDevice));
+    if (s->wide_copy_bytes) {
+      std::vector<Node128> wide(8 * nw);
+      for (uint32_t o = 0; o < 8; o++) {
+        const size_t copy = (size_t)o * nw;
+        auto rec_off = [&](size_t i) { return (uint32_t)(wide_base + (copy + i) * sizeof(Node128)); };
+        for (size_t i = 0; i < nw; i++) {
+          const Wide4& w = hs.wide[i];
+          Node128& r = wide[copy + i];
+          for (int k = 0; k < 4; k++) {
+            const int c = w.order[o][k];
+            memcpy(r.box[k], w.box[c], sizeof r.box[k]);
+            const uint32_t h = w.child[c];
+            if (c >= w.n) {
+              r.child[k] = kWideEmpty;
+              r.pf[k] = rec_off(i);
+            } else if (is_leaf(h)) {
+              r.child[k] = h;
+              r.pf[k] = (uint32_t)(64 * (nn + leaf_first(h)));
+            } else {
+              r.child[k] = rec_off(h);
+              r.pf[k] = rec_off(h);
+            }
+          }
+        }
+      }
+      HIPCHECK(hipMemcpy(reinterpret_cast<char*>(s->d_nodes) + wide_base, wide.data(), wide_bytes, hipMemcpyHostToDevice));
+    }
   }
   if ((rc = dalloc_copy(&s->d_nodes4, hs.nodes4.data(), hs.nodes4.size() * sizeof(Node4Q), tot))) return rc;
   {
@@ -2782,6 +3098,8 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.nodes4 = s->d_nodes4;
   P.sc.root4 = 0;
   P.sc.n_nodes4 = (int32_t)hs.nodes4.size();
+  P.sc.wide_base = s->wide_base;
+  P.sc.wide_copy_bytes = s->wide_copy_bytes;
   memcpy(P.sc.Minv, hs.Minv, 64);
   memcpy(P.Minv, hs.Minv, 64);
   memcpy(P.MS, hs.MS, 36);
@@ -2855,7 +3173,8 @@ static int ensure_fb(rt_scene::FrameSlot& f, size_t npix) {
 // 65536 = the generic traceRay kernel (k_render_depth) also at the modes' own depths; 131072 = the
 // default chunked-XCD dispatch order instead of longest-first (k_order_lpt); 262144 = longest-first
 // with half as many cost buckets (2 per octave: coarser, more spatial order kept); 524288 = longest-first
-// also while other frames are in flight.
+// also while other frames are in flight; 2097152 = PRIMARY packets on the binary tree instead of the fp32
+// 4-wide tree (traverse_wide_fast).
 // Default: binary nodes + LDS stack, FULL as one kernel (k_render_full) at the occupancy its scene
 // size selects.
 static int pick_trav(const FrameParams& P, int variant) {
@@ -3082,6 +3401,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   }
   const int grid = P.n_tiles_shard;
   const int variant = kernel_variant();
+  if (variant & 2097152) P.sc.wide_copy_bytes = 0;  // PRIMARY octant packets on the binary tree (A/B)
   // PRIMARY with two packets per wave (k_primary_dual): variant bit 1048576
   const bool dual = (fr->mode == RT_MODE_PRIMARY || fr->mode == RT_MODE_BOX_COLORS) && !stats &&
                     (fr->max_depth <= 1 || fr->mode == RT_MODE_BOX_COLORS) && !(variant & (1 | 2 | 4 | 32768 | 256 | 2048 | 65536)) &&
@@ -3329,7 +3649,8 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
       HIPCHECK(hipMemcpy(c, s->d_stats, sizeof c, hipMemcpyDeviceToHost));
       out->node_visits = (int64_t)c[ST_NODE];
       out->tri_tests = (int64_t)c[ST_TRI];
-      out->wave_node_fetches = (int64_t)c[ST_WNODE];
+      out->wave_node_fetches = (int64_t)(c[ST_WNODE] + c[ST_WWIDE]);
+      out->wave_node_bytes = (int64_t)(64 * c[ST_WNODE] + sizeof(Node128) * c[ST_WWIDE]);
       out->wave_tri_fetches = (int64_t)c[ST_WTRI];
       out->hits = (int64_t)c[ST_HITS];
       out->total_rays = (int64_t)c[ST_TOTAL];

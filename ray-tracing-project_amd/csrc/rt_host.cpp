@@ -553,6 +553,7 @@ extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
   o->max_boxes = INT32_MAX; // flyscene.hpp:169
   o->leaf_size = 0;
   o->frames_in_flight = 4;
+  o->builder = RT_BUILDER_SBVH;
   for (int k = 0; k < 3; k++) { o->default_material.ka[k] = 0.2f; o->background[k] = 0.9f; }
   o->default_material.kd[0] = 0.9f; o->default_material.kd[1] = 0.9f; o->default_material.kd[2] = 0.0f;
   o->default_material.shininess = 0.0f;
@@ -902,7 +903,7 @@ struct BvhBuilder {
 
 // Spatial-split BVH (SBVH: object splits as above, plus splits of the space that cut triangles
 // straddling the plane into two references with clipped bounds; the host builder's default when
-// RT_SBVH is not 0). A triangle referenced by several leaves is tested more than once, with
+// RT_BUILDER_SBVH). A triangle referenced by several leaves is tested more than once, with
 // identical (t, rank), so the (t, rank) argmin, hence every result, is unchanged; culling stays
 // conservative because each reference's box bounds the part of the triangle it stands for (clip
 // points in double, rounded outward) and every child box is padded as before.
@@ -1436,7 +1437,7 @@ static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, c
             hs.nf, nn);
 }
 
-void build_bvh(HostScene& hs, int leaf_size) {
+void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
   hs.nodes.clear();
   hs.tris.clear();
   hs.depth = 0;
@@ -1460,10 +1461,10 @@ void build_bvh(HostScene& hs, int leaf_size) {
   });
   Aabb world;
   for (int t = 0; t < TW; t++) world.merge(wparts[t]);
-  // spatial splits by default (RT_SBVH=<alpha>, 0 = the plain binned-SAH tree): alpha 1e-3 keeps the
-  // gain of 1e-5..1e-7 (the same node / triangle counts within 0.2%) at less than half the build time
-  static const float sbvh_alpha = [] { const char* e = getenv("RT_SBVH"); return e ? (float)atof(e) : 1e-3f; }();
-  if (sbvh_alpha > 0.0f && hs.nf > 1) { build_sbvh(hs, leaf_size, prims, world, sbvh_alpha); return; }
+  // spatial splits (RT_BUILDER_SBVH): alpha 1e-3 keeps the gain of 1e-5..1e-7 (the same node / triangle
+  // counts within 0.2%) at less than half the build time (profiles/ab/r02_sbvh_sweep.txt)
+  constexpr float kSbvhAlpha = 1e-3f;
+  if (spatial && hs.nf > 1) { build_sbvh(hs, leaf_size, prims, world, kSbvhAlpha); return; }
   std::vector<Node64> tmp((size_t)std::max(hs.nf, 1));
   BvhBuilder B{prims, tmp};
   B.hw = std::max(1u, std::thread::hardware_concurrency());
@@ -1632,6 +1633,85 @@ void build_bvh4(HostScene& hs) {
 }
 // (the wide traversal pushes at most 3 entries per level and writes up to 3 slots past the top)
 
+// ---------------------------------------------------------------------------------------------------
+// fp32 4-wide tree (Node128 on the device): the same collapse as above (each wide node opens the interior
+// child of largest surface area until it has four children), with the BVH2 child boxes kept exactly --
+// they are already padded, so culling stays conservative -- and, per ray-direction octant, the children's
+// near-to-far order. Order rule (the binary tree's octant_order, pairwise): of two children, along the
+// axis on which their centres are furthest apart, the one on the ray's entry side of that axis comes
+// first (insertion sort; only the visit order depends on it, never a result).
+// ---------------------------------------------------------------------------------------------------
+namespace {
+bool wide_before(const float* a, const float* b, uint32_t oct) {
+  int axis = 0;
+  float best = -1.0f;
+  for (int k = 0; k < 3; k++) {
+    const float sep = std::fabs((b[2 * k] + b[2 * k + 1]) - (a[2 * k] + a[2 * k + 1]));
+    if (sep > best) best = sep, axis = k;
+  }
+  const float ca = a[2 * axis] + a[2 * axis + 1], cb = b[2 * axis] + b[2 * axis + 1];
+  return ((oct >> axis) & 1u) ? ca > cb : ca < cb;
+}
+
+uint32_t collapse_wide(const std::vector<Node64>& bin, uint32_t n2, std::vector<Wide4>& out, int depth, int& maxd) {
+  maxd = std::max(maxd, depth);
+  WChild ch[4];
+  int n = 2;
+  child_box(bin[n2], 0, ch[0]);
+  child_box(bin[n2], 1, ch[1]);
+  if (ch[1].lo[0] > ch[1].hi[0]) n = 1;  // the never-hit sentinel child of a single-leaf root
+  while (n < 4) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int c = 0; c < n; c++)
+      if (!is_leaf(ch[c].h) && warea(ch[c]) > ba) { ba = warea(ch[c]); best = c; }
+    if (best < 0) break;
+    const Node64& sub = bin[ch[best].h];
+    WChild a, b;
+    child_box(sub, 0, a);
+    child_box(sub, 1, b);
+    ch[best] = a;
+    ch[n++] = b;
+  }
+  const uint32_t me = (uint32_t)out.size();
+  out.emplace_back();
+  uint32_t handles[4];
+  for (int c = 0; c < n; c++)
+    handles[c] = is_leaf(ch[c].h) ? ch[c].h : collapse_wide(bin, ch[c].h, out, depth + 1, maxd);
+  Wide4& w = out[me];
+  memset(&w, 0, sizeof w);
+  w.n = (uint8_t)n;
+  for (int c = 0; c < 4; c++) {
+    for (int k = 0; k < 3; k++) {
+      w.box[c][2 * k] = c < n ? ch[c].lo[k] : INFINITY;
+      w.box[c][2 * k + 1] = c < n ? ch[c].hi[k] : -INFINITY;
+    }
+    w.child[c] = c < n ? handles[c] : kWideEmpty;
+  }
+  for (uint32_t oct = 0; oct < 8; oct++) {
+    uint8_t* o = w.order[oct];
+    for (int c = 0; c < 4; c++) o[c] = (uint8_t)c;
+    for (int i = 1; i < n; i++)  // insertion sort of the occupied slots; empty slots stay last
+      for (int j = i; j > 0 && wide_before(w.box[o[j]], w.box[o[j - 1]], oct); j--) std::swap(o[j], o[j - 1]);
+  }
+  return me;
+}
+}  // namespace
+
+void build_wide(HostScene& hs) {
+  hs.wide.clear();
+  hs.depth_wide = 0;
+  if (hs.nodes.empty() || is_leaf(hs.root)) return;
+  hs.wide.reserve(hs.nodes.size() / 2 + 1);
+  int maxd = 0;
+  collapse_wide(hs.nodes, hs.root, hs.wide, 0, maxd);
+  hs.depth_wide = maxd + 1;
+  if (3 * hs.depth_wide + 4 > kStackW) {  // too deep for the wave stack: binary traversal only
+    hs.wide.clear();
+    hs.depth_wide = 0;
+  }
+}
+
 }  // namespace rt
 
 // =====================================================================================================
@@ -1736,10 +1816,13 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     if (built) s->builder_used = RT_BUILDER_LBVH_GPU;
   }
   if (!built) {
-    rt::build_bvh(hs, leaf);
+    const bool spatial = s->opts.builder == RT_BUILDER_SBVH;
+    rt::build_bvh(hs, leaf, spatial);
+    s->builder_used = spatial ? RT_BUILDER_SBVH : RT_BUILDER_SAH;
     if (getenv("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));
     rt::build_bvh4(hs);
   }
+  if (s->opts.wide_tree) rt::build_wide(hs);  // fp32 4-wide collapse of the binary tree (PRIMARY packets)
   s->bvh_ms = ms_since(t2);
   if (3 * hs.depth4 + 4 > rt::kStack4) hs.nodes4.clear();  // too deep for the wide stack: binary traversal
   if (hs.depth > rt::kMaxDepth + 2) {  // the wave stack holds 64 entries
@@ -1783,6 +1866,8 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->bvh_gpu_ms = s->bvh_gpu_ms;
   o->box_builder = s->box_builder_used;
   o->boxes_gpu_ms = s->boxes_gpu_ms;
+  o->wide_nodes = (int32_t)s->hs.wide.size();
+  o->wide_depth = s->hs.depth_wide;
   return RT_OK;
 }
 
@@ -1928,6 +2013,32 @@ struct Validator {
     }
     return all;
   }
+  // the fp32 4-wide tree (device Node128): its boxes are the binary tree's, copied; every octant order
+  // a permutation of the slots with the occupied ones first
+  std::vector<int> seenw;
+  VBox widef(uint32_t n, int d, int64_t& depth, const VBox& region) {
+    depth = std::max<int64_t>(depth, d + 1);
+    if (n >= hs.wide.size()) { bad++; return VBox{}; }
+    const rt::Wide4& w = hs.wide[n];
+    for (int o = 0; o < 8; o++) {
+      int mask = 0;
+      for (int k = 0; k < 4; k++) {
+        mask |= 1 << w.order[o][k];
+        if ((k < w.n) != (w.order[o][k] < w.n)) bad++;
+      }
+      if (mask != 15) bad++;
+    }
+    VBox all;
+    for (int c = 0; c < w.n; c++) {
+      const uint32_t h = w.child[c];
+      const double l[3] = {w.box[c][0], w.box[c][2], w.box[c][4]}, u[3] = {w.box[c][1], w.box[c][3], w.box[c][5]};
+      const VBox sub = cut(region, l, u);
+      const VBox b = rt::is_leaf(h) ? leaf(h, seenw, sub, false) : widef(h, d + 1, depth, sub);
+      if (!b.inside(l, u)) bad++;
+      all.add(b);
+    }
+    return all;
+  }
   // split trees: points of every face on a barycentric grid (vertices, edges, interior) each lie in
   // one of that face's leaf regions
   void coverage() {
@@ -1972,13 +2083,21 @@ extern "C" int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]) {
   if (!hs.nodes.empty()) v.bin(hs.root, 0, info[1], everywhere);
   if (!hs.nodes4.empty()) v.wide(0, 0, info[3], everywhere);
   if (!v.strict && !hs.nodes.empty()) v.coverage();
+  int64_t wide_depth = 0, wide_once = 0;
+  v.seenw.assign(hs.tris.size(), 0);
+  if (!hs.wide.empty()) {
+    v.widef(0, 0, wide_depth, everywhere);
+    if (wide_depth != hs.depth_wide || 3 * wide_depth + 4 > rt::kStackW) v.bad++;
+  }
   for (size_t i = 0; i < hs.tris.size(); i++) {
     info[4] += v.seen2[i] == 1;
     info[5] += v.seen4[i] == 1;
+    wide_once += v.seenw[i] == 1;
   }
   info[6] = v.bad;
   const bool ok = v.bad == 0 && info[4] == (int64_t)hs.tris.size() &&
-                  (hs.nodes4.empty() || info[5] == (int64_t)hs.tris.size());
+                  (hs.nodes4.empty() || info[5] == (int64_t)hs.tris.size()) &&
+                  (hs.wide.empty() || wide_once == (int64_t)hs.tris.size());
   if (!ok) { rt::set_error("acceleration structure check failed (%lld violations)", (long long)v.bad); return RT_ERR_INVALID; }
   return RT_OK;
 }

@@ -88,6 +88,21 @@ struct alignas(16) Node4Q {
 static_assert(sizeof(Node4Q) == 64, "wide node record must be 64 bytes");
 constexpr int kStack4 = 128;  // per-wave stack entries of the 4-wide traversal (needs 3 * depth4 + 4)
 
+// 4-wide node with exact fp32 child boxes (the default PRIMARY tree): one 128-B record, fetched per wave
+// with two s_load_dwordx16. The tree is stored once per ray-direction octant (8 copies), each copy with
+// every node's children in that octant's near-to-far order, so the traversal of a wave whose rays share
+// an octant visits the nearest hit child next and pushes the others farthest-first without sorting.
+struct alignas(128) Node128 {
+  float box[4][6];     // child c: lo.x hi.x lo.y hi.y lo.z hi.z (padded BVH2 boxes); empty slot: lo +inf, hi -inf
+  uint32_t child[4];   // interior: byte offset of the child's record (same copy) from the scene-record base;
+                       // leaf: leaf handle; empty slot: kWideEmpty (never entered by a certified ray)
+  uint32_t pf[4];      // byte offset of what the child's visit reads first (its record, or a leaf's first
+                       // triangle record): scalar-cache prefetch; empty slot: this record
+};
+static_assert(sizeof(Node128) == 128, "wide node record must be 128 bytes");
+constexpr uint32_t kWideEmpty = 0xFFFFFFFFu;  // = the traversal's pop marker: an entered empty slot pops
+constexpr int kStackW = 128;  // wave stack entries of the fp32 4-wide traversal (3 per level + 4 headroom)
+
 struct alignas(16) TriRec64 {
   float nx, ny, nz, dist;  // face.normal.normalized(), facenormal.dot(vert0)  (flyscene.cpp:450,459)
   float w0x, w0y, w0z, w1x;
@@ -116,6 +131,9 @@ struct DevScene {
   const Node4Q* nodes4;
   uint32_t root4;
   int32_t n_nodes4;
+  // fp32 4-wide tree (Node128), in the same allocation as `nodes`/`tris`: copy o's root record at byte
+  // offset wide_base + o * wide_copy_bytes from `nodes`; wide_base == 0: no wide tree (binary traversal)
+  uint32_t wide_base, wide_copy_bytes;
   const TriRec64* tris;
   const float* fshade;     // float4 x 3 per face: unit vertex normals (n0 .w = material id bits)
   const float* refbox;     // 2 float4 per box

@@ -26,6 +26,14 @@ struct RefBox {
   std::vector<int32_t> faces;
 };
 
+// One node of the fp32 4-wide tree before upload (device_upload lays out the eight octant copies)
+struct Wide4 {
+  float box[4][6];       // child boxes (lo.x hi.x lo.y hi.y lo.z hi.z), copied from the BVH2 node records
+  uint32_t child[4];     // wide-node index (interior) or leaf handle; slots >= n unused
+  uint8_t n;             // children (2..4; 1 only for a single-leaf root)
+  uint8_t order[8][4];   // per direction octant: child slots near to far
+};
+
 struct HostScene {
   int32_t nv = 0, nf = 0;
   std::vector<f3> wv;        // world vertices  (M * v)
@@ -41,7 +49,9 @@ struct HostScene {
   std::vector<uint32_t> face_rank, face_box;
   // BVH
   std::vector<Node64> nodes;
-  std::vector<Node4Q> nodes4;  // 4-wide collapse of `nodes`
+  std::vector<Node4Q> nodes4;  // 4-wide collapse of `nodes`, quantised boxes (A/B variant)
+  std::vector<Wide4> wide;     // 4-wide collapse of `nodes`, fp32 boxes (default PRIMARY tree); root = 0
+  int32_t depth_wide = 0;
   std::vector<TriRec64> tris;  // leaf order
   uint32_t root = 0;
   int32_t depth = 0, leaves = 0, depth4 = 0;
@@ -54,11 +64,12 @@ int gpu_build_ref_boxes(int device, HostScene& hs, const float* v4, int32_t min_
                         double* gpu_ms, bool* nonfinite);
 // face_rank / face_box from hs.boxes (boxes in creation order, faces in in-box order)
 void assign_box_ranks(HostScene& hs);
-void build_bvh(HostScene& hs, int leaf_size);
+void build_bvh(HostScene& hs, int leaf_size, bool spatial);  // spatial: SBVH (RT_BUILDER_SBVH)
 bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
 void build_bvh4(HostScene& hs);
+void build_wide(HostScene& hs);
 void set_error(const char* fmt, ...);
 
 }  // namespace rt
@@ -77,6 +88,7 @@ struct rt_scene {
   rt::Node64* d_nodes = nullptr;
   rt::Node4Q* d_nodes4 = nullptr;
   rt::TriRec64* d_tris = nullptr;
+  uint32_t wide_base = 0, wide_copy_bytes = 0;  // fp32 4-wide tree in d_nodes (DevScene), 0: none
   float* d_fshade = nullptr;  // per-face shading record: three unit vertex normals + material (float4 x 3)
   float* d_refbox = nullptr;
   // RT_MODE_BOX_COLORS: the boxes' colours and, per face id, the sum of the colours of the boxes that

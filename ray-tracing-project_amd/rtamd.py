@@ -50,7 +50,8 @@ class MeshDesc(C.Structure):
 class SceneOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("min_faces", C.c_int32), ("max_boxes", C.c_int32),
                 ("leaf_size", C.c_int32), ("default_material", Material), ("background", C.c_float * 3),
-                ("frames_in_flight", C.c_int32), ("builder", C.c_int32), ("box_builder", C.c_int32)]
+                ("frames_in_flight", C.c_int32), ("builder", C.c_int32), ("box_builder", C.c_int32),
+                ("wide_tree", C.c_int32)]
 
 
 class SceneInfo(C.Structure):
@@ -59,7 +60,7 @@ class SceneInfo(C.Structure):
                 ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("device", C.c_int32),
                 ("prep_ms", C.c_double), ("boxes_ms", C.c_double), ("bvh_ms", C.c_double), ("upload_ms", C.c_double),
                 ("builder", C.c_int32), ("bvh_gpu_ms", C.c_double), ("box_builder", C.c_int32),
-                ("boxes_gpu_ms", C.c_double)]
+                ("boxes_gpu_ms", C.c_double), ("wide_nodes", C.c_int32), ("wide_depth", C.c_int32)]
 
 
 class Camera(C.Structure):
@@ -92,7 +93,7 @@ class Stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("launches", C.c_int64), ("trace_kernel_ms", C.c_double),
                 ("primary_rays", C.c_int64), ("total_rays", C.c_int64),
                 ("hits", C.c_int64), ("node_visits", C.c_int64), ("tri_tests", C.c_int64),
-                ("wave_node_fetches", C.c_int64), ("wave_tri_fetches", C.c_int64)]
+                ("wave_node_fetches", C.c_int64), ("wave_tri_fetches", C.c_int64), ("wave_node_bytes", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -275,16 +276,17 @@ class Mesh:
             self.h = None
 
 
-RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU = 0, 1
+RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH = 0, 1, 2
 RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 
-def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=0,
-               box_builder=0):
+def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=2,
+               box_builder=0, wide_tree=0):
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
     o.builder = builder
     o.box_builder = box_builder
+    o.wide_tree = wide_tree
     if background is not None:
         o.background[:] = [float(x) for x in background]
     o.device = device
@@ -296,12 +298,12 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, backgr
 
 
 class Scene:
-    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=0,
-                 box_builder=0):
+    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=2,
+                 box_builder=0, wide_tree=0):
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
         self.h = C.c_void_p()
         d = mesh.desc()
-        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder, box_builder)
+        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder, box_builder, wide_tree)
         check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
 
     def info(self):

@@ -218,3 +218,23 @@ def test_gpu_lbvh_soup_matches_oracle_digests(rt, scenes):
     W, H = 1920, 1080
     rgb, face, t = gpu_frame(rt, lb, W, H, "primary")
     assert sha(face) == DIG["C3"]["face_sha256"] and sha(t) == DIG["C3"]["t_sha256"]
+
+
+@pytest.mark.parametrize("case,builder", [("C2", "sbvh"), ("C3", "sbvh"), ("C3", "sah"), ("C4", "sbvh")])
+def test_wide_tree_frames_match_oracle_digests(rt, scenes, case, builder):
+    """The fp32 4-wide tree (rt_scene_opts.wide_tree, traverse_wide_fast for PRIMARY octant packets;
+    mixed-octant packets on the binary tree) renders every pixel of C2 / C3 / C4 with the oracle's face
+    and t digests, over spatial-split and plain SAH trees; the counting run walks the same tree (node
+    visits drop, records are 128 B)."""
+    d = DIG[case]
+    mesh = scenes["bunny_mesh"] if d["scene"] == "bunny" else scenes["soup_mesh"]
+    b = rt.RT_BUILDER_SBVH if builder == "sbvh" else rt.RT_BUILDER_SAH
+    w = rt.Scene(mesh, builder=b, wide_tree=1)
+    info = w.info()
+    assert info["wide_nodes"] > 0 and info["builder"] == b
+    rgb, face, t = gpu_frame(rt, w, d["W"], d["H"], d["mode"])
+    assert sha(face) == d["face_sha256"] and sha(t) == d["t_sha256"], case
+    if case == "C3":
+        st = w.render(rt.flycam(d["W"], d["H"], 0, 0, 20), rt.DEFAULT_LIGHTS, d["W"], d["H"], flags=rt.RT_FRAME_STATS)[-1]
+        assert st["wave_node_bytes"] > 64 * 0 and st["wave_node_fetches"] > 0
+        assert st["wave_node_bytes"] > 64 * st["wave_node_fetches"]  # 128-B wide records dominate

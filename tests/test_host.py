@@ -20,7 +20,7 @@ def test_header_symbols_exported(rt):
     L = rt.lib()
     for name in sorted(decl):
         assert hasattr(L, name), name
-    assert L.rt_version() == 2
+    assert L.rt_version() == 3
     ident = rt.build_identity()
     assert ident["matches_tree"], ident
 
@@ -179,10 +179,13 @@ def test_bvh_trees_sound(rt, case):
                                    np.array([rt.SOUP_MATERIAL], np.float32))
     else:
         mesh = _soup(rt, 1 if case == "single" else 2)
-    sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
-    r = sc.validate_bvh()
+    sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE, wide_tree=1)
+    r = sc.validate_bvh()  # the fp32 4-wide tree too (violations count all three trees)
     assert r["ok"] and r["violations"] == 0, r
-    nf = sc.info()["n_faces"]
+    info = sc.info()
+    assert info["wide_nodes"] >= 1 or info["bvh_nodes"] <= 1
+    assert 3 * info["wide_depth"] + 4 <= 128
+    nf = info["n_faces"]
     # every triangle record in exactly one leaf; spatial splits may reference a face from several leaves
     # (the validator then checks that the faces' leaf regions cover them), within the reference budget
     assert nf <= r["covered2"] <= 1.5 * nf + 1 and r["covered4"] == r["covered2"]
@@ -331,6 +334,23 @@ def test_scene_cache_rejects_crafted_trees(rt, tmp_path):
     struct.pack_into("<i", s3[0], 36, 40)
     bad.write_bytes(_cache_sign(s3))
     assert rt.Scene.load(bad, device=rt.RT_DEVICE_NONE).info()["bvh_depth"] == 41
+    # 4. ADVICE r2: a face-less file (no triangles, no boxes) with one interior node and its root handle
+    # beyond the node table: rejected before the tree walk (which would index the node table with it)
+    s4 = [bytearray(x) for x in sec]
+    nv = struct.unpack_from("<i", s4[0], 16)[0]
+    rec = bytearray(sec[NODES][:64])
+    struct.pack_into("<II", rec, 48, 0, 0)  # both children: node 0 (interior)
+    s4[NODES] = rec
+    for k in range(4, 13):  # fnn, fdist, fidx, fmat, mats (kept), boxes, box faces, face_rank, face_box
+        if k != 8:
+            s4[k] = bytearray()
+    s4[NODES + 1] = bytearray()
+    s4[NODES + 2] = bytearray()
+    struct.pack_into("<8i", s4[0], 16, nv, 0, struct.unpack_from("<i", s4[0], 24)[0], 0, 0, 1, 0, 0)
+    struct.pack_into("<I", s4[0], 48, 7)  # root: node 7 of 1
+    bad.write_bytes(_cache_sign(s4))
+    with pytest.raises(rt.RTError, match="bad BVH root"):
+        rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
 
 
 def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
@@ -426,3 +446,22 @@ def test_face_limit_rejected_before_reading(rt):
         rc = rt.lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(h))
         assert rc != 0 and not h.value, n
         assert "face limit" in rt.lib().rt_last_error().decode()
+
+
+def test_builder_selected_through_abi(rt, tmp_path):
+    """the host tree's builder is a scene option (RT_BUILDER_SBVH default, RT_BUILDER_SAH
+    on request), reported in rt_scene_info and kept by the scene cache -- no environment variable."""
+    o = rt.SceneOpts()
+    rt.lib().rt_scene_opts_default(rt.C.byref(o))
+    assert o.builder == rt.RT_BUILDER_SBVH and o.wide_tree == 0
+    mesh = _soup(rt, 20_000)
+    sb = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
+    sa = rt.Scene(mesh, device=rt.RT_DEVICE_NONE, builder=rt.RT_BUILDER_SAH)
+    assert sb.info()["builder"] == rt.RT_BUILDER_SBVH and sa.info()["builder"] == rt.RT_BUILDER_SAH
+    assert sb.validate_bvh()["ok"] and sa.validate_bvh()["ok"]
+    # the spatial-split tree references clipped faces from several leaves; the SAH tree each face once
+    assert sa.validate_bvh()["covered2"] == 20_000 <= sb.validate_bvh()["covered2"]
+    for sc, b in ((sb, rt.RT_BUILDER_SBVH), (sa, rt.RT_BUILDER_SAH)):
+        p = tmp_path / f"b{b}.rtscene"
+        sc.save(p)
+        assert rt.Scene.load(p, device=rt.RT_DEVICE_NONE).info()["builder"] == b
