@@ -208,6 +208,17 @@ def make_reducer(dist, dev):
     return reduce
 
 
+def gather_all(dist, dev, x):
+    """Every rank's value of x, in rank order (timing metadata only)."""
+    import torch
+    if dist is None:
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    out = torch.zeros(dist.get_world_size(), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return [float(v) for v in out.tolist()]
+
+
 def same_build_profile(W, H, n_faces, mode, kernel, src_hash):
     """The committed rocprofv3 summary (profiles/pmc_latest.json, tools/profile.sh +
     tools/summarize_profile.py) when it was taken of this build (embedded source hash), this kernel and
@@ -228,6 +239,69 @@ def same_build_profile(W, H, n_faces, mode, kernel, src_hash):
     if why:
         return None, f"profiles/pmc_latest.json ({d.get('tag')}): " + ", ".join(why)
     return d, f"profiles/{d.get('tag')}_pmc.json"
+
+
+def shared_scene(build, load, rank, barrier, path):
+    """Rank 0 builds the scene and writes it to `path` (f1 scene cache); after a barrier every other rank
+    loads it; rank 0 removes the file once all have. Returns (scene, seconds): rank 0's build + save time,
+    the other ranks' load + upload time."""
+    t0 = time.perf_counter()
+    sc = None
+    if rank == 0:
+        sc = build()
+        sc.save(path)
+    setup_s = time.perf_counter() - t0
+    barrier()
+    if rank != 0:
+        t1 = time.perf_counter()
+        sc = load(path)
+        setup_s = time.perf_counter() - t1
+    barrier()
+    if rank == 0:
+        os.remove(path)
+    return sc, setup_s
+
+
+def kernel_bound(kernel):
+    """The limiter of `kernel` in the newest committed rocprofv3 summary (profiles/*_pmc.json, by file
+    time of the tag order): "latency", "hbm", "valu" or "salu" from its `limiter` text."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if not str(d.get("kernel", "")).startswith(kernel + "<") or not d.get("limiter"):
+            continue
+        if best is None or str(d.get("tag", "")) >= str(best[1].get("tag", "")):
+            best = (p, d)
+    if best is None:
+        return None, "no committed profile of " + kernel
+    lim = str(best[1]["limiter"]).split(":")[0].strip().lower()
+    return lim, f"profiles/{os.path.basename(best[0])}: {best[1]['limiter']}"
+
+
+def side_config(rt, scene_name, mode, steps, warmup, device):
+    """A single-GPU BASELINE config beside the headline one: C2 = bunny PRIMARY,
+    C5 = bunny FULL, 1920x1080: rate with frames in flight and one frame at a time."""
+    W, H = 1920, 1080
+    mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
+    m = rt.RT_MODE_FULL if mode == "full" else rt.RT_MODE_PRIMARY
+    cam = rt.flycam(W, H, 0, 0, 20)
+    out = {"workload": f"{scene_name}: Stanford bunny (69,451 triangles), {W}x{H} {mode}, eye (0,0,1), 1 light"}
+    for fif in (4, 1):
+        sc = rt.Scene(mesh, device=device, frames_in_flight=fif)
+        el, st = timed_frames(rt, sc, cam, W, H, m, (0, 1), steps, warmup, lambda: None, lambda: None)
+        key = "" if fif == 4 else "_one_frame_at_a_time"
+        out["mrays_per_s" + key] = round(st["primary_rays"] * steps / el / 1e6, 2)
+        out["ms_per_frame" + key] = round(el / steps * 1e3, 4)
+        if fif == 4:
+            sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, flags=rt.RT_FRAME_STATS)
+            s2 = sc.synchronize()
+            out["total_mrays_per_s"] = round(s2["total_rays"] * steps / el / 1e6, 2)
+        del sc
+    return out
 
 
 def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_device):
@@ -278,6 +352,9 @@ def main():
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + 8-bit frame to host) timing")
     ap.add_argument("--no-extra", action="store_true", help="skip the second frame size (c4_frame / c3_frame)")
+    ap.add_argument("--no-side", action="store_true", help="skip the C2 / C5 lines of the N=1 run")
+    ap.add_argument("--no-shared-build", action="store_true",
+                    help="N > 1: every rank builds the scene itself instead of loading rank 0's scene cache")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
     ap.add_argument("--builder", choices=["sbvh", "sah", "lbvh"], default="sbvh",
                     help="BVH builder: host SAH with spatial splits (default), host binned SAH, or the device LBVH "
@@ -332,17 +409,35 @@ def main():
     W, H = frame_for(K or n, a.frame)
     t0 = time.perf_counter()
     if a.scene == "soup":
-        mesh, _, _ = rt.soup_mesh(a.tris, 12345)
         scene_name = f"{a.tris} random triangles (SplitMix64 seed 12345)"
     else:
-        mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         scene_name = "Stanford bunny (69,451 triangles)"
-    sc = rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight,
-                  builder={"lbvh": rt.RT_BUILDER_LBVH_GPU, "sah": rt.RT_BUILDER_SAH, "sbvh": rt.RT_BUILDER_SBVH}[a.builder],
-                  wide_tree=1 if a.wide else 0)
+    builder = {"lbvh": rt.RT_BUILDER_LBVH_GPU, "sah": rt.RT_BUILDER_SAH, "sbvh": rt.RT_BUILDER_SBVH}[a.builder]
+
+    def build_scene():
+        if a.scene == "soup":
+            mesh, _, _ = rt.soup_mesh(a.tris, 12345)
+        else:
+            mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
+        return rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight, builder=builder,
+                        wide_tree=1 if a.wide else 0)
+
+    # N > 1 (one node): the scene is built once -- rank 0 builds it and writes the f1 scene cache
+    # (rt_scene_save), the other ranks load it (rt_scene_load: no OBJ parse, no box partition, no BVH
+    # build) -- instead of every rank building the same tree on the shared host
+    cache_path = None
+    if world > 1 and not a.no_shared_build:
+        cache_path = os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                  f"rtamd_{a.scene}_{a.tris}_{a.builder}_{a.leaf}_{os.environ.get('MASTER_PORT', '0')}.rtscene")
+        sc, setup_s = shared_scene(
+            build_scene, lambda p: rt.Scene.load(p, device=local, frames_in_flight=a.frames_in_flight,
+                                                 wide_tree=1 if a.wide else 0), rank, barrier, cache_path)
+    else:
+        sc = build_scene()
+        setup_s = time.perf_counter() - t0
     info = sc.info()
     info_fif = a.frames_in_flight or 4
-    setup_s = time.perf_counter() - t0
+    setup_per_rank = gather_all(dist, dev, setup_s)
     cam = rt.flycam(W, H, 0, 0, 20)
     mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY
     shard = (0, K) if K else (rank, n)
@@ -372,6 +467,12 @@ def main():
         extra = {"frame": f"{W2}x{H2}", "workload": "C4 frame on 1 GPU" if n == 1 else f"C3 frame split over {n} GPUs",
                  "mrays_per_s": round(rays2 / el2 / 1e6, 2), "ms_per_step": round(el2 / k2 * 1e3, 4), "steps": k2}
 
+    # the other single-GPU BASELINE configs on the same GPU (N = 1 headline run only)
+    side = {}
+    if n == 1 and not a.no_side and a.frame is None and a.scene == "soup" and a.mode == "primary" and not K:
+        for cn, md in (("c2", "primary"), ("c5", "full")):
+            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local)
+
     roof = None
     stats = None
     if rank == 0 and not a.no_stats:
@@ -398,7 +499,11 @@ def main():
                 traffic = round(traffic_b / (kern_ms * 1e-3) / 1e9, 1)
             issue = prof.get("issue")
             limiter = prof.get("limiter")
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        # what bounds the kernel, as the newest committed profile of it measured: the
+        # roofline below is still priced against HBM bandwidth, the resource north_star names
+        bound, bound_src = kernel_bound(kname)
+        roof = {"bound": bound, "bound_source": bound_src, "priced_against": "hbm",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "traffic_bytes_per_launch": traffic_b, "traffic_source": prof_src,
                 "kernel": kname, "kernel_ms_isolated": round(kern_ms, 4),
@@ -467,6 +572,8 @@ def main():
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
                        "wide_tree": {"nodes_per_copy": info["wide_nodes"], "depth": info["wide_depth"]} if info["wide_nodes"] else None,
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
+                       "scene_setup_s_per_rank": [round(x, 2) for x in setup_per_rank],
+                       "scene_shared_build": cache_path is not None,
                        "builder": {0: "sah-host", 1: "lbvh-gpu", 2: "sbvh-host"}.get(info["builder"], str(info["builder"])),
                        "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
                                     "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),
@@ -477,6 +584,7 @@ def main():
         }
         if extra is not None:
             out["c4_frame" if n == 1 else "c3_frame"] = extra
+        out.update(side)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -185,14 +185,18 @@ __device__ __forceinline__ float nudge(float x) { return fabsf(x) < 1e-20f ? cop
 #define RT_DYN_PAD 1
 #endif
 constexpr float kCullPadRel = 4e-5f, kCullOriginMax = 1e18f, kCullDirMin = 1e-12f, kCullDirMax = 1e18f;
-__device__ __forceinline__ void setup_cull(Ray& r) {
+// The ray's own pad is needed only once it exceeds the static one (every box already carries
+// static_pad >= the ray's pad, so the same ~100x margin holds): for origins near the scene -- every
+// secondary ray, and primary rays of an eye near it -- the boxes keep exactly their static size.
+__device__ __forceinline__ void setup_cull(Ray& r, float static_pad) {
   const float om = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
   const float dm = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
   const bool certified = !RT_DYN_PAD || (om <= kCullOriginMax && dm >= kCullDirMin && dm <= kCullDirMax);  // false for NaN
   if (certified) {
     r.id = f3{__builtin_amdgcn_rcpf(nudge(r.d.x)), __builtin_amdgcn_rcpf(nudge(r.d.y)),
               __builtin_amdgcn_rcpf(nudge(r.d.z))};
-    const float p = RT_DYN_PAD ? kCullPadRel * om : 0.0f;
+    const float pr = kCullPadRel * om;
+    const float p = RT_DYN_PAD && pr > static_pad ? pr : 0.0f;
     r.oa = f3{-(r.o.x + p) * r.id.x, -(r.o.y + p) * r.id.y, -(r.o.z + p) * r.id.z};
     r.ob = f3{-(r.o.x - p) * r.id.x, -(r.o.y - p) * r.id.y, -(r.o.z - p) * r.id.z};
   } else {
@@ -1481,9 +1485,45 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
 #endif
 // WIDE: packets whose rays share an octant walk the fp32 4-wide tree when the scene has one
 // (traverse_wide_fast; the counting run traverse_wide); mixed-octant packets keep the binary loop.
-template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false, bool WIDE = false>
+// SPLIT (FULL mode's secondary packets, RT_FULL_SPLIT_OCT): a packet whose rays span several direction
+// octants is walked once per octant present, each walk with that octant's lanes only (ballot masks) and
+// the octant loop's cheaper slab test, instead of one generic walk of the union; a one-octant packet is
+// the loop's single iteration. Each lane is traced by exactly one walk, so results are unchanged.
+template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false, bool WIDE = false, bool SPLIT = false>
 __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                           WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
+  if (SPLIT && RT_OCT_SPECIALIZE && RT_FAST_LOOP && !STATS && TRAV == TRAV_B2_LDS) {
+    const uint32_t loct = (__float_as_uint(r.id.x) >> 31) | ((__float_as_uint(r.id.y) >> 31) << 1) |
+                          ((__float_as_uint(r.id.z) >> 31) << 2);
+    uint64_t rem = ballot(active);
+    Hit hres = h;
+    bool fres = found;
+    while (rem != 0) {
+      const uint32_t oct = uniform((uint32_t)__builtin_amdgcn_readlane((int)loct, (int)__builtin_ctzll(rem)));
+      const uint64_t sub = ballot(loct == oct) & rem;
+      rem &= ~sub;
+      const bool a = lane_in(sub);
+      Hit hs = h;
+      bool fs = false;
+      switch (oct) {
+        case 0: traverse_fast<ANY, 0>(P, r, a, hs, fs, L.stack[wv]); break;
+        case 1: traverse_fast<ANY, 1>(P, r, a, hs, fs, L.stack[wv]); break;
+        case 2: traverse_fast<ANY, 2>(P, r, a, hs, fs, L.stack[wv]); break;
+        case 3: traverse_fast<ANY, 3>(P, r, a, hs, fs, L.stack[wv]); break;
+        case 4: traverse_fast<ANY, 4>(P, r, a, hs, fs, L.stack[wv]); break;
+        case 5: traverse_fast<ANY, 5>(P, r, a, hs, fs, L.stack[wv]); break;
+        case 6: traverse_fast<ANY, 6>(P, r, a, hs, fs, L.stack[wv]); break;
+        default: traverse_fast<ANY, 7>(P, r, a, hs, fs, L.stack[wv]); break;
+      }
+      hres.t = a ? hs.t : hres.t;
+      hres.rank = a ? hs.rank : hres.rank;
+      hres.slot = a ? hs.slot : hres.slot;
+      fres = fres | (a & fs);
+    }
+    h = hres;
+    found = fres;
+    return;
+  }
   if (RT_OCT_SPECIALIZE && (TRAV == TRAV_B2_LDS || TRAV == TRAV_B2_VGPR)) {
     constexpr bool SL = TRAV == TRAV_B2_LDS;
     const uint64_t act = ballot(active);
@@ -1562,6 +1602,9 @@ __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& 
 #endif
 #ifndef RT_FULL_OCT_REFL  // the reflection packet through trace_oct (octant loops when its rays share one)
 #define RT_FULL_OCT_REFL 1
+#endif
+#ifndef RT_FULL_SPLIT_OCT  // FULL secondary packets spanning several octants: one octant walk per octant
+#define RT_FULL_SPLIT_OCT 1       // present (small-scene build; trace_full)
 #endif
 // RT_FULL_LANE_K > 0: a secondary packet with at most K active lanes walks per lane (traverse_lane)
 // instead of as a packet (A/B knob)
@@ -1666,7 +1709,7 @@ __device__ __forceinline__ float clamp01(float x) { return smax(smin(x, 1.0f), 0
 
 // calculateColor (flyscene.cpp:603-614). SHADOWS: per light, a wave-packet any-hit traversal from
 // P + 0.003 L (box predicate from P) decides whether the light contributes (calcSingleColor :543).
-template <bool SHADOWS, bool STATS, int TRAV, bool OCTSH = false>
+template <bool SHADOWS, bool STATS, int TRAV, bool OCTSH = false, bool SPLIT = false>
 __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, const HitInfo& hi, f3 o, bool lane_hit,
                                          WaveLds<TRAV, STATS>* lds, int wv, uint32_t* cnt) {
   f3 sum{0.0f, 0.0f, 0.0f};
@@ -1680,10 +1723,11 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       sr.d = L;
       sr.o2 = affv3(P.Minv, hi.p);
       sr.d2 = normalized(m3v3(P.MS, L));
-      setup_cull(sr);
+      setup_cull(sr, P.sc.static_pad);
       Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if (STATS && lane_hit) cnt[ST_TOTAL]++;
-      if (OCTSH) trace_oct<true, STATS, TRAV, RT_FULL_MIXED_LANE != 0>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
+      if (OCTSH)
+        trace_oct<true, STATS, TRAV, RT_FULL_MIXED_LANE != 0, false, SPLIT>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
       else trace_full_ray<true, STATS, TRAV>(P.sc, sr, lane_hit, hh, blocked, *lds, wv, cnt);
     }
     f3 c{0.0f, 0.0f, 0.0f};
@@ -1783,7 +1827,7 @@ __device__ __forceinline__ Ray primary_ray(const FrameParams& P, int px, int py)
   r.d = normalized(sub(w, r.o));
   r.o2 = f3{P.eye_obj[0], P.eye_obj[1], P.eye_obj[2]};
   r.d2 = normalized(m3v3(P.MS, r.d));
-  setup_cull(r);
+  setup_cull(r, P.sc.static_pad);
   return r;
 }
 
@@ -2212,7 +2256,10 @@ void k_primary_dual(FrameParams P) {
 // traceRay(o, d, 0) with max_depth 2 (FULL, flyscene.cpp:317-371): primary hit, per-light shadows, one
 // reflection bounce with its own shadows. Shared by the frame megakernel and the ray-list colour query.
 // Returns the colour; h0 / face0: the first hit (t, face id).
-template <bool STATS, int TRAV>
+// SPLIT: mixed-octant secondary packets walk once per octant (trace_oct); the small-scene build only --
+// measured C5 +1.5% at 4 frames in flight, +1..3% one at a time, the 1M soup in FULL -5%
+// (profiles/ab/r03_full_split_oct_ab.txt)
+template <bool STATS, int TRAV, bool SPLIT = false>
 __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, bool active, WaveLds<TRAV, STATS>& lds, int wv,
                                          uint32_t* cnt, Hit& h, uint32_t& face0) {
   h = Hit{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -2237,7 +2284,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   }
   // the primary hits' shadow packets head for the same light from neighbouring points: octant loops for
   // them too (A/B knob RT_FULL_OCT_SHADOW); the reflection hits' shadows keep the generic loop
-  const f3 direct0 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW != 0>(P, st, hi0, r.o, hit0, &lds, wv, cnt);
+  const f3 direct0 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW != 0, SPLIT>(P, st, hi0, r.o, hit0, &lds, wv, cnt);
   if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
 
   // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
@@ -2247,10 +2294,11 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   rr.o = offset(hi0.p, rr.d, 0.001f);
   rr.o2 = affv3(P.Minv, rr.o);
   rr.d2 = normalized(m3v3(P.MS, rr.d));
-  setup_cull(rr);
+  setup_cull(rr, P.sc.static_pad);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  if (RT_FULL_OCT_REFL) trace_oct<false, STATS, TRAV, RT_FULL_MIXED_LANE != 0>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
+  if (RT_FULL_OCT_REFL)
+    trace_oct<false, STATS, TRAV, RT_FULL_MIXED_LANE != 0, false, SPLIT>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   else trace_full_ray<false, STATS, TRAV>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
@@ -2263,7 +2311,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
     hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
     hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
   }
-  const f3 direct1 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW2 != 0>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
+  const f3 direct1 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW2 != 0, SPLIT>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
   if (hit1) {
     if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
     // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped
@@ -2326,7 +2374,7 @@ __device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r
       rr.o = offset(hi.p, rr.d, 0.001f);
       rr.o2 = affv3(P.Minv, rr.o);
       rr.d2 = normalized(m3v3(P.MS, rr.d));
-      setup_cull(rr);
+      setup_cull(rr, P.sc.static_pad);
       if (STATS && hit) cnt[ST_TOTAL]++;
       cur = rr;
       act = hit;
@@ -2372,7 +2420,8 @@ void k_render_full(FrameParams P) {
   Hit h;
   uint32_t face0;
   const f3 col = RT_FULL_LOOP ? trace_full_loop<STATS, TRAV>(P, r, active, lds, c.slot, cnt, h, face0)
-                              : trace_full<STATS, TRAV>(P, r, active, lds, c.slot, cnt, h, face0);
+                              : trace_full<STATS, TRAV, RT_FULL_SPLIT_OCT != 0 && WPE == RT_FULL_WAVES_PER_EU_SMALL>(
+                                    P, r, active, lds, c.slot, cnt, h, face0);
   const bool hit0 = face0 != 0xFFFFFFFFu;
   if (active) {
     const size_t pix = (size_t)c.py * P.W + c.px;
@@ -2454,7 +2503,7 @@ void k_render_depth(FrameParams P) {
     rr.o = offset(hi.p, rr.d, 0.001f);
     rr.o2 = affv3(P.Minv, rr.o);
     rr.d2 = normalized(m3v3(P.MS, rr.d));
-    setup_cull(rr);
+    setup_cull(rr, P.sc.static_pad);
     if (STATS && hit) cnt[ST_TOTAL]++;
     cur = rr;
     act = hit;
@@ -2614,7 +2663,7 @@ void k_full_shadow(FrameParams P, int pass) {
     sr.d = Ld;
     sr.o2 = affv3(P.Minv, p);
     sr.d2 = normalized(m3v3(P.MS, Ld));
-    setup_cull(sr);
+    setup_cull(sr, P.sc.static_pad);
     Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
     bool blocked = false;
     if (STATS && L.act) cnt[ST_TOTAL]++;
@@ -2644,7 +2693,7 @@ void k_full_refl(FrameParams P) {
   rr.o = f3{rq.ox, rq.oy, rq.oz};
   rr.o2 = affv3(P.Minv, rr.o);
   rr.d2 = normalized(m3v3(P.MS, rr.d));
-  setup_cull(rr);
+  setup_cull(rr, P.sc.static_pad);
   uint32_t cnt[ST_COUNT] = {};
   if (STATS && L.act) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -2758,7 +2807,7 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
     r.o2 = affv3(P.Minv, r.o);
   }
   r.d2 = normalized(m3v3(P.MS, r.d));
-  setup_cull(r);
+  setup_cull(r, P.sc.static_pad);
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool found = false;
   trace<ANY, false, TRAV>(P.sc, r, active, h, found, lds, (int)uniform(threadIdx.x >> 6), nullptr);
@@ -2806,7 +2855,7 @@ void k_rays_color(FrameParams P, RayParams R) {
   r.d = ld3(R.d + 3 * (size_t)j);
   r.o2 = affv3(P.Minv, r.o);
   r.d2 = normalized(m3v3(P.MS, r.d));
-  setup_cull(r);
+  setup_cull(r, P.sc.static_pad);
   Hit h;
   uint32_t face0;
   const f3 col = trace_full<false, TRAV>(P, r, active, lds, wv, nullptr, h, face0);
@@ -2922,6 +2971,7 @@ int device_upload(rt_scene* s) {
   int64_t& tot = s->device_bytes;
   tot = 0;
   int rc;
+  s->static_pad = scene_static_pad(hs);
   {
     // BVH nodes and triangle records share one allocation (triangles right after the nodes), so one
     // base plus a 32-bit byte offset reaches either: with RT_PREFETCH each uploaded node's pad0 / pad1
@@ -3098,6 +3148,7 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.nodes4 = s->d_nodes4;
   P.sc.root4 = 0;
   P.sc.n_nodes4 = (int32_t)hs.nodes4.size();
+  P.sc.static_pad = s->static_pad;
   P.sc.wide_base = s->wide_base;
   P.sc.wide_copy_bytes = s->wide_copy_bytes;
   memcpy(P.sc.Minv, hs.Minv, 64);

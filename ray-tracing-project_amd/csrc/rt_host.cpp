@@ -1231,13 +1231,24 @@ static bool safe_normal(const HostScene& hs, uint32_t f) {
 
 // conservative padding of every BVH child box: covers the reference's rounding of P = o + t d and of
 // the inclusive edge tests for ray origins within ~16 scene extents (DESIGN.md "Exactness of culling")
-static float bvh_pad(const float lo[3], const float hi[3]) {
+float bvh_pad(const float lo[3], const float hi[3]) {
   float ext = 0.0f, mag = 0.0f;
   for (int k = 0; k < 3; k++) {
     ext = std::max(ext, hi[k] - lo[k]);
     mag = std::max(mag, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
   }
   return 2e-5f * std::max(std::max(ext, mag), 1e-3f);
+}
+
+// the static pad the builders gave every box: bvh_pad of the triangles' bounds (the builders' `world`)
+float scene_static_pad(const HostScene& hs) {
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (const TriRec64& t : hs.tris) {
+    const float v[9] = {t.w0x, t.w0y, t.w0z, t.w1x, t.w1y, t.w1z, t.w2x, t.w2y, t.w2z};
+    for (int j = 0; j < 3; j++)
+      for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], v[3 * j + k]); hi[k] = std::max(hi[k], v[3 * j + k]); }
+  }
+  return hs.tris.empty() ? 0.0f : bvh_pad(lo, hi);
 }
 
 void world_bounds(const HostScene& hs, float lo[3], float hi[3]) {

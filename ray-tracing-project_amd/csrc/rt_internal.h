@@ -134,6 +134,7 @@ struct DevScene {
   // fp32 4-wide tree (Node128), in the same allocation as `nodes`/`tris`: copy o's root record at byte
   // offset wide_base + o * wide_copy_bytes from `nodes`; wide_base == 0: no wide tree (binary traversal)
   uint32_t wide_base, wide_copy_bytes;
+  float static_pad;        // the pad every BVH box carries (setup_cull adds a ray's own pad beyond it)
   const TriRec64* tris;
   const float* fshade;     // float4 x 3 per face: unit vertex normals (n0 .w = material id bits)
   const float* refbox;     // 2 float4 per box

@@ -383,12 +383,12 @@ class Scene:
         check(lib().rt_scene_save(self.h, os.fsencode(path)))
 
     @classmethod
-    def load(cls, path, device=-1, frames_in_flight=0):
+    def load(cls, path, device=-1, frames_in_flight=0, wide_tree=0):
         """Scene from a binary cache (rt_scene_load): no OBJ parsing, no builds."""
         self = cls.__new__(cls)
         self.mesh = None
         self.h = C.c_void_p()
-        o = scene_opts(device, 300, 0, frames_in_flight)
+        o = scene_opts(device, 300, 0, frames_in_flight, wide_tree=wide_tree)
         check(lib().rt_scene_load(os.fsencode(path), C.byref(o), C.byref(self.h)))
         return self
 

@@ -106,3 +106,38 @@ def test_sharded_renders_stitch_to_full_frame(orc):
         for (x, y), c in zip(pix, rgb):
             out[y, x] = c
     assert out.tobytes() == full.reshape(H, W, 3).tobytes()
+
+
+def _shared_worker(rank, world, port, path, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import conftest
+    rt = conftest.rtamd
+    mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
+    sc, secs = bench.shared_scene(lambda: rt.Scene(mesh, device=rt.RT_DEVICE_NONE),
+                                  lambda p: rt.Scene.load(p, device=rt.RT_DEVICE_NONE), rank, dist.barrier, path)
+    info = sc.info()
+    per_rank = bench.gather_all(dist, torch.device("cpu"), secs)
+    q.put((rank, info["bvh_nodes"], info["n_ref_boxes"], info["builder"], sc.validate_bvh()["ok"], per_rank))
+    dist.destroy_process_group()
+
+
+def test_gloo_scene_built_once_per_node(tmp_path):
+    """with N > 1 ranks on one node, rank 0 builds the scene and writes the f1 cache,
+    the others load it (bench.shared_scene); every rank ends up with the same tree, and the cache file
+    is removed afterwards."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "shared.rtscene")
+    procs = [ctx.Process(target=_shared_worker, args=(r, 3, port, path, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len({r[1:4] for r in res}) == 1 and all(r[4] for r in res)
+    assert res[0][3] == 2  # RT_BUILDER_SBVH, kept by the cache
+    assert len(res[0][5]) == 3 and all(x >= 0 for x in res[0][5])
+    assert not os.path.exists(path)

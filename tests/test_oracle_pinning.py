@@ -2,6 +2,9 @@
 
   * tests/golden/eigen_kat.bin: every Eigen 3.3.7 float expression of the hot path, evaluated by the
     reference's vendored Eigen (oracle/eigen_kat.cpp) -- the oracle must reproduce every bit;
+  * tests/golden/tucano_kat.bin: the camera (getCenter, screenToWorld) and model-matrix
+    (normalizeModelMatrix) known answers computed by the reference's own Tucano code, compiled
+    unmodified (oracle/tucano_kat.cpp, no GL library linked);
   * tests/golden/survey_kat.json: values printed by the unmodified reference at survey time
      -- ray directions (bits), hit distances, colours, box counts and the
     per-pass box sequence of generateBoundingBoxes.
@@ -15,8 +18,8 @@ import pytest
 from conftest import GOLDEN, scene_path
 
 
-def read_kat():
-    raw = open(os.path.join(GOLDEN, "eigen_kat.bin"), "rb").read()
+def _read_kat_file(name):
+    raw = open(os.path.join(GOLDEN, name), "rb").read()
     magic, count = np.frombuffer(raw[:8], np.uint32)
     assert magic == 0x4B54414B
     off, secs = 8, []
@@ -29,6 +32,27 @@ def read_kat():
         off += 4 * n * ol
         secs.append((op, n, il, ol, inp, exp))
     return secs
+
+
+def read_kat():
+    """Known answers: the Eigen expressions from eigen_kat.bin (the reference's vendored Eigen), with the
+    camera / model-matrix ops (SHAPE 8, CENTER 15, SCREEN 16) taken from tucano_kat.bin -- computed by the
+    reference's own Tucano::Camera / Tucano::Model code (oracle/tucano_kat.cpp)."""
+    tucano = {s[0]: s for s in _read_kat_file("tucano_kat.bin")}
+    return [tucano.get(s[0], s) for s in _read_kat_file("eigen_kat.bin")]
+
+
+def test_tucano_kat_from_reference_code_equals_eigen_kat():
+    """The reference's Tucano::Camera::getCenter / screenToWorld and Model::normalizeModelMatrix (compiled
+    unmodified, oracle/tucano_kat.cpp) give exactly the bits of eigen_kat.cpp's restated formulas, on the
+    same 2,000 inputs per op."""
+    eig = {s[0]: s for s in _read_kat_file("eigen_kat.bin")}
+    tuc = _read_kat_file("tucano_kat.bin")
+    assert sorted(s[0] for s in tuc) == [8, 15, 16]
+    for op, n, il, ol, inp, exp in tuc:
+        e = eig[op]
+        assert (n, il, ol) == e[1:4] and inp.tobytes() == e[4].tobytes()
+        assert exp.view(np.uint32).tolist() == e[5].view(np.uint32).tolist(), op
 
 
 def same_bits(a, b):
