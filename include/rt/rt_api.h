@@ -307,9 +307,13 @@ int rt_frame_unpack_shards_rgb8(const void* packed_device, int32_t shard_count, 
 
 /* Box colours of RT_MODE_BOX_COLORS. The reference draws them in generateBoundingBoxes when its
  * RENDER_BOUNDINGBOX_COLORED_TRIANGLES flag is set (flyscene.cpp:422-427): BoundingBox::setRandomColor
- * per box in creation order, colour = (rand() / (float)RAND_MAX) x 3 (BoundingBox.cpp:163-165).
+ * per box in creation order, colour = Vector3f(rand() / (float)RAND_MAX, x3) (BoundingBox.cpp:163-165).
  * rt_box_colors_random reproduces that sequence from rng (NULL = seed 1: a fresh reference process,
- * whose first rand() calls these are) into out3 [n_boxes][3]. rt_scene_set_box_colors gives the scene
+ * whose first rand() calls these are) into out3 [n_boxes][3], with the constructor's arguments
+ * evaluated right to left as the reference's g++ (and x86-64 MSVC) build does: each box's first
+ * rand() call is its blue channel, the third its red (C++ leaves the order unspecified; pinned by
+ * tests/golden/boxcolor_kat.bin from that expression compiled here). Callers of another compiler's
+ * order pass their own colours to rt_scene_set_box_colors. rt_scene_set_box_colors gives the scene
  * its colours ([n_ref_boxes][3]; NULL = rt_box_colors_random(n_ref_boxes, NULL)); a scene that renders
  * RT_MODE_BOX_COLORS without them gets the NULL colours. The per-face sums are computed on the device
  * at the first box-colour frame after the colours change (one pass over faces x boxes). */

@@ -1103,9 +1103,15 @@ int orc_render(orc_scene* s, const orc_camera* cam, const float* lights, int32_t
   return 0;
 }
 
+/* BoundingBox::setRandomColor (BoundingBox.cpp:163-165) per box in creation order, as the reference built
+ * with g++ evaluates Vector3f(rand()/RAND_MAX, x3): arguments right to left, so a box's first rand() call
+ * is its blue channel (pinned by tests/golden/boxcolor_kat.bin, oracle/boxcolor_kat.cpp) */
 void orc_box_colors_glibc(int32_t n, float* out3) {
   srand(1);
-  for (int32_t i = 0; i < 3 * n; i++) out3[i] = rand() / (float)RAND_MAX;
+  for (int32_t i = 0; i < n; i++) {
+    const float c2 = rand() / (float)RAND_MAX, c1 = rand() / (float)RAND_MAX, c0 = rand() / (float)RAND_MAX;
+    out3[3 * i] = c0; out3[3 * i + 1] = c1; out3[3 * i + 2] = c2;
+  }
 }
 
 int orc_closest(orc_scene* s, int32_t n, const float* o, const float* d, int32_t* face, float* t, float* P) {

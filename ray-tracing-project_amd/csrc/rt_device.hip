@@ -1856,9 +1856,10 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
   struct { uint64_t t0; uint32_t r0; } w;
   w.t0 = (uint64_t)uniform(clk[0]) | ((uint64_t)uniform(clk[1]) << 32);
   w.r0 = uniform(clk[2]);
-  // this wave's cost for the next frame's dispatch order; a split sub-wave leaves the whole wave's cost
-  // from an earlier frame in place (it ranked the wave among the costliest; the sub-wave's own time
-  // would not)
+  // this wave's cost for the next frame's dispatch order. Frames that record costs (P.cost: the order's
+  // first frame and every kLptRefresh-th) run whole waves (split_k = 0), so every wave's cost is
+  // re-measured on the same basis; keep_cost is a guard for a sub-wave, whose own time would not rank
+  // the whole wave
   if (P.cost && lane == 0 && !keep_cost) {
     const uint64_t dt = t1 - w.t0;
     P.cost[qw] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
@@ -3355,14 +3356,10 @@ extern "C" int rt_device_count(void) {
 // pixels) per super-tile when the frame is split, so that the waves an XCD runs together trace
 // neighbouring pixels (the rank's L2 working set stays compact): C4 over 8 / 4 GPUs +10% / +7% per GPU
 // against single tiles interleaved (profiles/ab/r02_super_tiles_ab.txt); an unsplit frame keeps its tile
-// order (super-tiles there: C3 ±1%, C4 -3%). RT_SUPER_TILE (A/B) overrides it inside the library; the
-// shard-tile helpers (rt_frame_shard_tiles, pack / unpack, rt_frame_shard_bytes) follow the same rule.
-static int frame_super_tile(int shard_count) {
-  static const int env = [] { const char* e = getenv("RT_SUPER_TILE"); return e ? atoi(e) : 0; }();
-  if (kernel_variant() & 16) return 1;  // the FULL stage pipeline sizes its lists by the frame's own tiles
-  if (env > 0) return env;
-  return shard_count > 1 ? kShardSuperTile : 1;
-}
+// order (super-tiles there: C3 +-1%, C4 -3%). A pure function of the shard count: the render,
+// rt_frame_shard_tiles, the pack on every rank and the unpack on rank 0 derive the same layout, whatever
+// the process environment or the kernel variant.
+static int frame_super_tile(int shard_count) { return shard_count > 1 ? kShardSuperTile : 1; }
 
 extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
                                const rt_frame* fr) {
@@ -3473,6 +3470,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
     s->last_timeline_waves = (int64_t)waves;
   }
   if (fr->mode == RT_MODE_FULL && (variant & 16)) {
+    if (sc > 1) { set_error("rt_render: the FULL stage-pipeline variant renders whole frames only"); return RT_ERR_UNSUPPORTED; }
     // sized by the 16x16-padded frame: every wave of the tile grid has a count slot
     const size_t npad = (size_t)P.tiles_x * 16 * (size_t)P.tiles_y * 16;
     if ((rc = ensure_full(slot, npad))) return rc;
@@ -3573,7 +3571,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       // (RT_SPLIT_KP waves)
       static const int split_p = [] { const char* e = getenv("RT_SPLIT_KP"); return e ? atoi(e) : kSplitKPrimary; }();
       const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
-      P.split_k = (P.order && small_p && !P.timeline && RT_TRACE_WPB == 1)
+      P.split_k = (P.order && !P.cost && small_p && !P.timeline && RT_TRACE_WPB == 1)
                       ? std::max(0, std::min<int>(split_p, (int)(units / 4))) & ~7 : 0;
       const dim3 g(grid * (4 / RT_TRACE_WPB) + 3 * P.split_k), b(64 * RT_TRACE_WPB);
       // RT_LDS_PAD (diagnostics): extra dynamic LDS per block, to cap the resident waves per CU in
@@ -3624,7 +3622,9 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       // per SIMD on the soup) and the extra waves only cost (-6%), so it keeps whole waves. Results do not
       // depend on the grouping (exact per-lane culling, (t, rank) argmin).
       static const int split_env = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atoi(e) : kSplitK; }();
-      if (P.order && small && !P.timeline && !stats && RT_FULL_WPB == 1 && trav == TRAV_B2_LDS)
+      // Cost-recording frames (P.cost) keep whole waves so the costliest waves' costs are refreshed too
+      // (a split wave's sub-waves do not write one).
+      if (P.order && !P.cost && small && !P.timeline && !stats && RT_FULL_WPB == 1 && trav == TRAV_B2_LDS)
         P.split_k = std::max(0, std::min<int>(split_env, (int)(units / 4))) & ~7;
       else
         P.split_k = 0;

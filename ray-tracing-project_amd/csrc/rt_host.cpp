@@ -912,8 +912,7 @@ struct SbvhBuilder {
   std::vector<Node64>& nodes;                      // sized to the node capacity
   std::vector<std::vector<uint32_t>> leaf_lists;   // face ids per leaf, sized to the leaf capacity
   std::atomic<uint32_t> next{0}, nleaf{0};
-  std::atomic<int64_t> refs{0};
-  int64_t ref_budget = 0;
+  std::atomic<int64_t> refs{0};  // references made (statistics); the budget itself is per subtree
   int leaf_size = 4;
   float pad = 0.0f, kTrav = 0.7f, alpha = 1e-5f, root_area = 1.0f;
   std::atomic<int> max_depth{0};
@@ -1029,8 +1028,11 @@ struct SbvhBuilder {
     }
   }
 
-  // builds the subtree over `r` (consumed); returns its handle and the bounds of its references
-  uint32_t build(std::vector<Prim>& r, int depth, Aabb& box) {
+  // builds the subtree over `r` (consumed); returns its handle and the bounds of its references.
+  // budget: references this subtree may add by spatial splits. Each split spends what it duplicates and
+  // hands the rest to its children in proportion to their reference counts, so the tree (which splits
+  // are taken) never depends on the order the parallel subtree tasks run in.
+  uint32_t build(std::vector<Prim>& r, int depth, Aabb& box, int64_t budget) {
     const uint32_t n = (uint32_t)r.size();
     Aabb cb;
     box = Aabb();
@@ -1083,7 +1085,7 @@ struct SbvhBuilder {
       for (int k = 0; k < 3; k++) d[k] = std::max(0.0f, std::min(o_lb.hi[k], o_rb.hi[k]) - std::max(o_lb.lo[k], o_rb.lo[k]));
       ov = 2.0f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
     }
-    if (!forced && refs.load() < ref_budget && (o_axis < 0 || ov > alpha * root_area)) {
+    if (!forced && budget > 0 && (o_axis < 0 || ov > alpha * root_area)) {
       float w[3];
       for (int k = 0; k < 3; k++) {
         w[k] = (box.hi[k] - box.lo[k]) / kBins;
@@ -1134,9 +1136,10 @@ struct SbvhBuilder {
       });
       int64_t straddle = 0;
       for (int t = 0; t < T; t++) straddle += cnt[t];
-      if (refs.fetch_add(straddle) + straddle > ref_budget) {
-        refs -= straddle;
-        spatial = false;
+      if (straddle > budget) spatial = false;
+      else {
+        budget -= straddle;
+        refs += straddle;
       }
     }
     if (spatial || o_axis >= 0) {
@@ -1175,16 +1178,17 @@ struct SbvhBuilder {
     }
     std::vector<Prim>().swap(r);
     const uint32_t me = next.fetch_add(1);
+    const int64_t bl = (int64_t)((double)budget * (double)L.size() / (double)(L.size() + R.size())), br = budget - bl;
     Aabb lb, rb;
     uint32_t lh, rh;
     if (n > 4096 && depth < 16 && take_task(tasks, hw)) {
-      auto fut = std::async(std::launch::async, [&]() { return build(L, depth + 1, lb); });
-      rh = build(R, depth + 1, rb);
+      auto fut = std::async(std::launch::async, [&]() { return build(L, depth + 1, lb, bl); });
+      rh = build(R, depth + 1, rb, br);
       lh = fut.get();
       tasks.fetch_sub(1);
     } else {
-      lh = build(L, depth + 1, lb);
-      rh = build(R, depth + 1, rb);
+      lh = build(L, depth + 1, lb, bl);
+      rh = build(R, depth + 1, rb, br);
     }
     Node64 nd{};
     set_child(nd, 0, lb, lh);
@@ -1396,7 +1400,6 @@ static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, c
   SbvhBuilder B{hs, tmp};
   B.hw = std::max(1u, std::thread::hardware_concurrency());
   B.leaf_lists.resize((size_t)cap);
-  B.ref_budget = cap;
   B.refs = hs.nf;
   B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
   if (const char* e = getenv("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
@@ -1405,7 +1408,7 @@ static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, c
   B.root_area = std::max(world.area(), 1e-30f);
   Aabb rootb;
   const auto tb0 = std::chrono::steady_clock::now();
-  uint32_t root = B.build(prims, 0, rootb);
+  uint32_t root = B.build(prims, 0, rootb, cap - hs.nf);
   uint32_t nn = B.next.load();
   if (is_leaf(root)) {
     Node64 nd{};
@@ -1882,12 +1885,16 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   return RT_OK;
 }
 
-// BoundingBox::setRandomColor (BoundingBox.cpp:163-165) per box in creation order
+// BoundingBox::setRandomColor (BoundingBox.cpp:163-165) per box in creation order. The three rand() calls
+// are constructor arguments, whose evaluation order C++ leaves open; the reference built with g++ (this
+// image's compiler, and x86-64 MSVC alike) evaluates them right to left: a box's first call is its blue
+// channel (tests/golden/boxcolor_kat.bin, generated from that expression by oracle/boxcolor_kat.cpp).
 extern "C" int rt_box_colors_random(int32_t n_boxes, rt_rand_state* rng, float* out3) {
   if (n_boxes < 0 || (n_boxes && !out3)) { rt::set_error("rt_box_colors_random: bad arguments"); return RT_ERR_INVALID; }
   rt_rand_state local;
   if (!rng) { rt_rand_seed(&local, 1); rng = &local; }
-  for (int64_t i = 0; i < 3 * (int64_t)n_boxes; i++) out3[i] = (float)rt_rand(rng) / (float)2147483647;
+  for (int64_t b = 0; b < (int64_t)n_boxes; b++)
+    for (int k = 2; k >= 0; k--) out3[3 * b + k] = (float)rt_rand(rng) / (float)2147483647;
   return RT_OK;
 }
 

@@ -367,15 +367,19 @@ def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
 
 def test_box_colors_random_matches_glibc(rt, orc):
     """RENDER_BOUNDINGBOX_COLORED_TRIANGLES colours: setRandomColor per box in creation order
-    (BoundingBox.cpp:163-165) = rand() / (float)RAND_MAX from the C library's own srand(1) + rand()."""
+    (BoundingBox.cpp:163-165) = Vector3f(rand() / (float)RAND_MAX, x3) from the C library's own srand(1) +
+    rand(), the constructor's arguments evaluated as g++ compiles the reference's expression (right to
+    left: tests/golden/boxcolor_kat.bin from oracle/boxcolor_kat.cpp)."""
+    kat = np.fromfile(os.path.join(GOLDEN, "boxcolor_kat.bin"), np.float32).reshape(-1, 3)
     got = rt.box_colors_random(4480)
+    assert got.tobytes() == kat.tobytes()
     assert got.tobytes() == orc.box_colors_glibc(4480).tobytes()
     r = rt.Rand(7)
     a = rt.box_colors_random(10, r)
     b = rt.box_colors_random(10, r)  # the state advances: 30 rand() calls per 10 boxes
     r2 = rt.Rand(7)
-    seq = np.array([r2() for _ in range(60)], np.float32) / np.float32(2147483647)
-    assert np.concatenate([a, b]).reshape(-1).tobytes() == seq.tobytes()
+    seq = np.array([r2() for _ in range(60)], np.float32).reshape(-1, 3)[:, ::-1] / np.float32(2147483647)
+    assert np.concatenate([a, b]).reshape(-1).tobytes() == np.ascontiguousarray(seq).reshape(-1).tobytes()
 
 
 def test_scene_box_colors_arguments(rt):
@@ -465,3 +469,17 @@ def test_builder_selected_through_abi(rt, tmp_path):
         p = tmp_path / f"b{b}.rtscene"
         sc.save(p)
         assert rt.Scene.load(p, device=rt.RT_DEVICE_NONE).info()["builder"] == b
+
+
+def test_sbvh_build_is_deterministic(rt, tmp_path):
+    """the spatial-split builder's reference budget is shared out per subtree, so the tree does
+    not depend on the order its parallel subtree tasks run in: two builds save byte-identical caches."""
+    mesh = _soup(rt, 200_000)
+    paths = []
+    for k in range(2):
+        sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
+        assert sc.info()["builder"] == rt.RT_BUILDER_SBVH
+        p = tmp_path / f"s{k}.rtscene"
+        sc.save(p)
+        paths.append(p)
+    assert paths[0].read_bytes() == paths[1].read_bytes()
