@@ -1849,20 +1849,31 @@ __device__ __forceinline__ void wave_clock_start(const FrameParams& P, uint32_t*
     }
   }
 }
+// RT_SUBWAVE_COST: how a split wave's cost is refreshed -- 0 kept from the frame that measured it whole,
+// 1 sum of its sub-waves' times, 2 their maximum, 3 cost-recording frames run whole waves (no split)
+#ifndef RT_SUBWAVE_COST
+#define RT_SUBWAVE_COST 2
+#endif
 __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint32_t* clk, int lane, int qw,
-                                               bool keep_cost = false) {
+                                               bool sub_wave = false) {
   if (!RT_WAVE_CLOCK || (!P.timeline && !P.cost)) return;
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   struct { uint64_t t0; uint32_t r0; } w;
   w.t0 = (uint64_t)uniform(clk[0]) | ((uint64_t)uniform(clk[1]) << 32);
   w.r0 = uniform(clk[2]);
-  // this wave's cost for the next frame's dispatch order. Frames that record costs (P.cost: the order's
-  // first frame and every kLptRefresh-th) run whole waves (split_k = 0), so every wave's cost is
-  // re-measured on the same basis; keep_cost is a guard for a sub-wave, whose own time would not rank
-  // the whole wave
-  if (P.cost && lane == 0 && !keep_cost) {
+  // this wave's cost for the next frame's dispatch order. The four 16-lane sub-waves of a split wave
+  // (sub_wave) write the maximum of their times into the wave's slot, which the host cleared before such
+  // a frame (RT_SUBWAVE_COST 2): a split wave's cost is re-measured like every other wave's, so one whose
+  // work has become cheap leaves the split range (profiles/ab/r03_subwave_cost_ab.txt: the sum ranks the
+  // split waves far above the rest and coarsens the order's buckets, -20% on C5 lone frames; keeping the
+  // stale cost is within 1% of the maximum but never refreshes it; running cost-recording frames unsplit
+  // costs 6%)
+  if (P.cost && lane == 0) {
     const uint64_t dt = t1 - w.t0;
-    P.cost[qw] = dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt;
+    const uint32_t c = dt > 0x3FFFFFFFull ? 0x3FFFFFFFu : (uint32_t)dt;
+    if (!sub_wave) P.cost[qw] = c;
+    else if (RT_SUBWAVE_COST == 1) atomicAdd(P.cost + qw, c);
+    else if (RT_SUBWAVE_COST == 2) atomicMax(P.cost + qw, c);
   }
   if (!P.timeline) return;
   const uint32_t r1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -3571,8 +3582,11 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       // (RT_SPLIT_KP waves)
       static const int split_p = [] { const char* e = getenv("RT_SPLIT_KP"); return e ? atoi(e) : kSplitKPrimary; }();
       const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
-      P.split_k = (P.order && !P.cost && small_p && !P.timeline && RT_TRACE_WPB == 1)
+      P.split_k = (P.order && small_p && !P.timeline && RT_TRACE_WPB == 1)
                       ? std::max(0, std::min<int>(split_p, (int)(units / 4))) & ~7 : 0;
+      if (P.cost && RT_SUBWAVE_COST == 3) P.split_k = 0;
+      if (P.cost && P.split_k && (RT_SUBWAVE_COST == 1 || RT_SUBWAVE_COST == 2))
+        HIPCHECK(hipMemsetAsync(P.cost, 0, units * 4, st));  // sub-waves add / take the max
       const dim3 g(grid * (4 / RT_TRACE_WPB) + 3 * P.split_k), b(64 * RT_TRACE_WPB);
       // RT_LDS_PAD (diagnostics): extra dynamic LDS per block, to cap the resident waves per CU in
       // occupancy experiments (160 KiB / (pad + 1 KiB) blocks per CU)
@@ -3622,12 +3636,13 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       // per SIMD on the soup) and the extra waves only cost (-6%), so it keeps whole waves. Results do not
       // depend on the grouping (exact per-lane culling, (t, rank) argmin).
       static const int split_env = [] { const char* e = getenv("RT_SPLIT_K"); return e ? atoi(e) : kSplitK; }();
-      // Cost-recording frames (P.cost) keep whole waves so the costliest waves' costs are refreshed too
-      // (a split wave's sub-waves do not write one).
-      if (P.order && !P.cost && small && !P.timeline && !stats && RT_FULL_WPB == 1 && trav == TRAV_B2_LDS)
+      if (P.order && small && !P.timeline && !stats && RT_FULL_WPB == 1 && trav == TRAV_B2_LDS)
         P.split_k = std::max(0, std::min<int>(split_env, (int)(units / 4))) & ~7;
       else
         P.split_k = 0;
+      if (P.cost && RT_SUBWAVE_COST == 3) P.split_k = 0;
+      if (P.cost && P.split_k && (RT_SUBWAVE_COST == 1 || RT_SUBWAVE_COST == 2))
+        HIPCHECK(hipMemsetAsync(P.cost, 0, units * 4, st));  // sub-waves add / take the max
       if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav, small); else launch_full<true, false>(P, grid, st, trav, small); }
       else { if (hits) launch_full<false, true>(P, grid, st, trav, small); else launch_full<false, false>(P, grid, st, trav, small); }
       HIPCHECK(hipEventRecord(ev_m, st));

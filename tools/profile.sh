@@ -8,7 +8,7 @@ OUT=${OUTDIR:-gpurun_out/prof}
 mkdir -p $OUT
 # one frame on the GPU at a time, so that each dispatch's duration is the duration its counters saw
 # (clock = GRBM_GUI_ACTIVE / 8 / duration); only the bench frame's launches (no second frame size)
-ARGS="${BENCH_ARGS:---steps 20 --warmup 5 --no-cpu --no-extra --no-e2e --frames-in-flight 1}"
+ARGS="${BENCH_ARGS:---steps 20 --warmup 5 --no-cpu --no-extra --no-e2e --no-side --frames-in-flight 1}"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_avail.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
     python3 bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace.err
@@ -20,7 +20,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ
            ${EXTRA_PMC:-}; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set -d $OUT/pmc$i -o run --output-format csv -- \
-      python3 bench.py ${PMC_ARGS:---steps 5 --warmup 1 --no-cpu --no-stats --no-extra --no-e2e --frames-in-flight 1} > $OUT/pmc$i.json 2> $OUT/pmc$i.err
+      python3 bench.py ${PMC_ARGS:---steps 5 --warmup 1 --no-cpu --no-stats --no-extra --no-e2e --no-side --frames-in-flight 1} > $OUT/pmc$i.json 2> $OUT/pmc$i.err
   rc=$?; echo "pmc$i ($set) rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac
 done
