@@ -126,6 +126,30 @@ __device__ __forceinline__ Node64 sload_node_pf_carry(const Node64* base, uint32
   __builtin_memcpy(&r, &v, 64);
   return r;
 }
+// RT_PF_INREG: the same carried prefetch, with the child offsets read from the node record's own
+// registers (Node64::pad0 / pad1, words 14 / 15 of the x16 load) instead of two extra one-dword loads:
+// two scalar-memory instructions fewer per node step. The prefetch is a second asm right after the
+// load's wait; the ray's reciprocal direction, passed through it as a read-write operand (a loop-carried
+// copy, no move), keeps the box tests below it.
+#ifndef RT_PF_INREG
+#define RT_PF_INREG 1
+#endif
+__device__ __forceinline__ Node64 sload_node_pf_inreg(const Node64* base, uint32_t h, uint32_t& pf0, uint32_t& pf1,
+                                                      f3& id) {
+  const uint32_t off = node_offset(__builtin_amdgcn_readfirstlane(h));
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  i16v v;
+  asm volatile("s_load_dwordx16 %0, %3, %4\n\ts_waitcnt lgkmcnt(0)" : "=&s"(v), "+s"(pf0), "+s"(pf1) : "s"(bs), "s"(off) : "memory");
+  Node64 r;
+  __builtin_memcpy(&r, &v, 64);
+  asm volatile("s_load_dword %0, %5, %6\n\ts_load_dword %1, %5, %7"
+               : "+s"(pf0), "+s"(pf1), "+v"(id.x), "+v"(id.y), "+v"(id.z)
+               : "s"(bs), "s"(r.pad0), "s"(r.pad1)
+               : "memory");
+  return r;
+}
 __device__ __forceinline__ TriRec64 sload_tri(const TriRec64* base, uint32_t i) { return sload64(base, i); }
 // node fetch by byte offset with one carried prefetch sink (RT_PF_MODE 1 / 2: the step's own s_waitcnt
 // retires the previous step's far-child prefetch)
@@ -235,7 +259,11 @@ __device__ __forceinline__ Span slab(float lx, float hx, float ly, float hy, flo
 #ifndef RT_CLIP_ASM
 #define RT_CLIP_ASM 1
 #endif
-template <int OCT>
+// CLIP = false (octant loops of packets whose rays all start in front of the scene, trace_oct): the entry
+// distance is not clipped at 0. That admits a superset of boxes (max(tmin, 0) >= tmin), so culling stays
+// conservative, and for such a packet it admits no extra box: every box lies inside the root's, which
+// each ray enters at t >= 0 or misses, and the rounded plane distances are monotone in the coordinates.
+template <int OCT, bool CLIP = true>
 __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
                                        float tmax_ray) {
   if (OCT < 0) return slab(lx, hx, ly, hy, lz, hz, r, tmax_ray);
@@ -247,8 +275,12 @@ __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, f
   const float noy = (OCT & 2) ? r.ob.y : r.oa.y, foy = (OCT & 2) ? r.oa.y : r.ob.y;
   const float noz = (OCT & 4) ? r.ob.z : r.oa.z, foz = (OCT & 4) ? r.oa.z : r.ob.z;
   Span s;
-  s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
-                 fmaxf(__builtin_fmaf(nz, r.id.z, noz), 0.0f));
+  if (CLIP)
+    s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
+                   fmaxf(__builtin_fmaf(nz, r.id.z, noz), 0.0f));
+  else
+    s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
+                   __builtin_fmaf(nz, r.id.z, noz));
 #if RT_CLIP_ASM
   // min of the three far planes and tmax_ray in two instructions (the compiler's fminf would first
   // canonicalise tmax_ray, a loop-carried value, with an extra v_max per node)
@@ -325,6 +357,9 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
 // calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record, for the lanes of
 // `act`. CLOSEST: update (t, rank, slot) if 0 <= t < best (rank breaks ties as the reference's order
 // does). ANY: any valid t >= 0 (shadow(), flyscene.cpp:519).
+#ifndef RT_TRI_CLASS  // 1: the closest-hit candidate range test as one v_cmp_class (same set)
+#define RT_TRI_CLASS 1
+#endif
 template <bool ANY>
 __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, uint32_t slot, const Ray& r,
                                          uint64_t act, Hit& h, bool& found) {
@@ -332,10 +367,20 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
   const float dn = dot(n, r.d);                 // facenormal.dot(dir)
   const float orth = tr.dist - dot(r.o, n);     // distancePlane - origin.dot(facenormal)
   const float t = orth / dn;                    // / dir.dot(facenormal)  (same bits as dn)
-  uint64_t cand = act & fmask<kFcmpUNE>(dn, 0.0f) & fmask<kFcmpOGE>(t, 0.0f);
-  if (!ANY)
-    cand &= fmask<kFcmpOLT>(t, INFINITY) &
-            (fmask<kFcmpOLT>(t, h.t) | (fmask<kFcmpOEQ>(t, h.t) & __builtin_amdgcn_uicmp(tr.rank, h.rank, kIcmpULT)));
+  uint64_t cand;
+  if (!ANY && RT_TRI_CLASS) {
+    // dn != 0 && 0 <= t < inf in one class test: t is -0, +0, +denormal or +normal (dn == 0 makes t
+    // +-inf or NaN, which the class excludes as the separate tests did)
+    uint64_t cls;
+    asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(cls) : "v"(t), "v"(0x1E0u));
+    cand = act & cls &
+           (fmask<kFcmpOLT>(t, h.t) | (fmask<kFcmpOEQ>(t, h.t) & __builtin_amdgcn_uicmp(tr.rank, h.rank, kIcmpULT)));
+  } else {
+    cand = act & fmask<kFcmpUNE>(dn, 0.0f) & fmask<kFcmpOGE>(t, 0.0f);
+    if (!ANY)
+      cand &= fmask<kFcmpOLT>(t, INFINITY) &
+              (fmask<kFcmpOLT>(t, h.t) | (fmask<kFcmpOEQ>(t, h.t) & __builtin_amdgcn_uicmp(tr.rank, h.rank, kIcmpULT)));
+  }
   if (cand == 0) return;
   const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
@@ -550,6 +595,9 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kPopMarker = 0xFFFFFFFFu;
 
+#ifndef RT_DECIDE8  // 1: the octant loops' post-mask decision in 8 SALU instead of 9 (same result)
+#define RT_DECIDE8 1
+#endif
 #ifndef RT_EARLY_PUSH
 #define RT_EARLY_PUSH 1
 #endif
@@ -559,10 +607,33 @@ __device__ __forceinline__ void lds_push(uint32_t* slot, uint32_t v) {
   const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)slot;
   asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+// RT_STACK_ASM (A/B, off: the compiler pads the inline asm with s_nop wait states, a net loss): the push / pop address base + 4 sp in one VALU op (v_lshl_add_u32 with the depth as its
+// scalar operand) instead of a scalar shift plus a move into a VGPR
+#ifndef RT_STACK_ASM
+#define RT_STACK_ASM 0
+#endif
+__device__ __forceinline__ uint32_t lds_base(const uint32_t* stack) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)stack;
+}
+__device__ __forceinline__ void lds_push_at(const uint32_t* stack, uint32_t sp, uint32_t v) {
+  // one asm: the address op separates the scalar write of v (the caller's s_cselect) from its move
+  // into a VGPR, so no wait state is needed between them
+  uint32_t a, d;
+  asm volatile("v_lshl_add_u32 %0, %2, 2, %3\n\tv_mov_b32 %1, %4\n\tds_write_b32 %0, %1"
+               : "=&v"(a), "=&v"(d)
+               : "s"(sp), "v"(lds_base(stack)), "s"(v)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_pop_at(const uint32_t* stack, uint32_t sp) {
+  uint32_t a, v;
+  asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "s"(sp), "v"(lds_base(stack)));
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
 
 // traverse_fast from a given state (node handle, stack depth): the whole traversal starts at the root
 // with an empty stack; the dual-chain loop (traverse_dual) hands over a half-finished one
-template <bool ANY, int OCT>
+template <bool ANY, int OCT, bool CLIP = true>
 __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                                    uint32_t* lds_stack, uint32_t node, int sp) {
   uint64_t act = ballot(active);  // lanes still tracing: used by the triangle tests only
@@ -574,6 +645,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
   uint32_t fsink = 0;  // RT_PF_MODE 1 / 3 / 4: the scalar prefetch's sink
   uint32_t vsink0 = 0, vsink1 = 0;  // RT_PF_MODE 4 / 5: the vector prefetches' sinks
   uint32_t tos = 0;  // RT_TOS: lds_stack[sp - 1] while sp > 0
+  f3 rid = r.id;  // RT_PF_INREG: loop-carried copy threaded through the prefetch asm
   for (;;) {
     while (!is_leaf(node)) {
       const int sp_before = sp;
@@ -581,6 +653,8 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
 #if RT_PF_MODE != 0
       // 1: the far child is prefetched after the decision, only when it is pushed; 2: no prefetch
       const Node64 nd = sload_node_sink(P.nodes, node, fsink);
+#elif RT_PREFETCH && RT_PF_CARRY && RT_PF_INREG
+      const Node64 nd = sload_node_pf_inreg(P.nodes, node, cpf0, cpf1, rid);
 #elif RT_PREFETCH && RT_PF_CARRY
       const Node64 nd = sload_node_pf_carry(P.nodes, node, cpf0, cpf1);
 #elif RT_PREFETCH
@@ -613,7 +687,8 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
             : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [c0] "s"(uniform(nd.child0)),
               [c1] "s"(uniform(nd.child1))
             : "scc");
-        lds_push(lds_stack + sp, farb);
+        if (RT_STACK_ASM) lds_push_at(lds_stack, (uint32_t)sp, farb);
+        else lds_push(lds_stack + sp, farb);
       }
       if ((RT_PF_MODE == 4 || RT_PF_MODE == 5) && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
         // 4: the far child's line into L2 by one vector load (its own counter: no scalar wait is tied to
@@ -658,8 +733,14 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
             : "scc");
       }
       const float tcut = ANY ? tlim : h.t;
-      const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
-      const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
+#if RT_PREFETCH && RT_PF_CARRY && RT_PF_INREG && RT_PF_MODE == 0
+      Ray rb = r;
+      rb.id = rid;
+#else
+      const Ray& rb = r;
+#endif
+      const Span s0 = slab_o<OCT, CLIP>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, rb, tcut);
+      const Span s1 = slab_o<OCT, CLIP>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, rb, tcut);
       const uint64_t m0 = mask_le(s0.tmin, s0.tmax), m1 = mask_le(s1.tmin, s1.tmax);
       uint32_t nxt, far, ta, tb;
       uint64_t tt;
@@ -669,6 +750,12 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
       // decision block values it keeps in VGPRs; readfirstlane folds away on SGPR values)
       sp = (int)uniform((uint32_t)sp);
       const uint32_t c0 = uniform(nd.child0), c1 = uniform(nd.child1);
+#if defined(RT_EXP_NODE_VALU)  // timing experiment only: N extra VALU per node step
+      { uint32_t xv = c0; asm volatile(".rept " RT_STR(RT_EXP_NODE_VALU) "\n\tv_add_u32 %0, %0, 1\n\t.endr" : "+v"(xv)); }
+#endif
+#if defined(RT_EXP_NODE_SALU)  // timing experiment only: N extra SALU per node step
+      { uint32_t xs = c0; asm volatile(".rept " RT_STR(RT_EXP_NODE_SALU) "\n\ts_add_u32 %0, %0, 1\n\t.endr" : "+s"(xs) :: "scc"); }
+#endif
 #if RT_VADDR_PUSH
       // the push address scaled in a VALU op (the scalar unit is the loop's tighter resource)
       uint32_t vsp = (uint32_t)sp;
@@ -679,6 +766,20 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
 #endif
       if (RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
         // both needed: the near child chosen above; one needed: that one; none: the pop marker
+#if RT_DECIDE8
+        // 8 SALU: any1 picks (c1 | pop) and (near | c0), any0 then chooses between them; both -> push
+        asm("s_cmp_lg_u64 %[m1], 0\n\t"
+            "s_cselect_b32 %[nxt], %[c1], -1\n\t"
+            "s_cselect_b32 %[ta], %[nb], %[c0]\n\t"
+            "s_cselect_b64 %[tt], %[m0], 0\n\t"
+            "s_cmp_lg_u64 %[m0], 0\n\t"
+            "s_cselect_b32 %[nxt], %[ta], %[nxt]\n\t"
+            "s_cmp_lg_u64 %[tt], 0\n\t"
+            "s_addc_u32 %[sp], %[sp], 0"
+            : [nxt] "=&s"(nxt), [sp] "+s"(sp), [tt] "=&s"(tt), [ta] "=&s"(ta)
+            : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [nb] "s"(nearb)
+            : "scc");
+#else
         asm("s_cmp_lg_u64 %[m1], 0\n\t"
             "s_cselect_b32 %[nxt], %[nb], %[c0]\n\t"
             "s_cmp_eq_u64 %[m0], 0\n\t"
@@ -691,6 +792,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
             : [nxt] "=&s"(nxt), [sp] "+s"(sp), [tt] "=&s"(tt)
             : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [nb] "s"(nearb)
             : "scc");
+#endif
         far = farb;
         (void)ta;
         (void)tb;
@@ -791,6 +893,11 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
       for (uint32_t k = 0; k < count; k++) {
         const TriRec64 tr = sload_tri(P.tris, first + k);
         test_tri<ANY>(P, tr, first + k, r, act, h, found);
+#if defined(RT_EXP_TRI_TWICE)  // timing experiment only: each triangle tested again (no effect on results)
+        TriRec64 t2 = tr;
+        asm volatile("" : "+s"(t2.nx), "+s"(t2.ny), "+s"(t2.nz), "+s"(t2.dist));
+        test_tri<ANY>(P, t2, first + k, r, act, h, found);
+#endif
       }
 #if RT_PREFETCH >= 3
       asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(q1), "s"(q2), "s"(q3), "s"(q4) : "memory");
@@ -812,7 +919,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
       node = uniform(tos);
       tos = lds_stack[sp > 0 ? sp - 1 : 0];
     } else {
-      node = uniform(lds_stack[sp]);
+      node = RT_STACK_ASM ? lds_pop_at(lds_stack, (uint32_t)sp) : uniform(lds_stack[sp]);
     }
   }
 #if RT_PREFETCH && RT_PF_CARRY
@@ -823,11 +930,11 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
   if (!ANY && !active) h.t = INFINITY;
 }
 
-template <bool ANY, int OCT>
+template <bool ANY, int OCT, bool CLIP = true>
 __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                               uint32_t* lds_stack) {
   if (P.n_nodes == 0) return;
-  traverse_fast_from<ANY, OCT>(P, r, active, h, found, lds_stack, P.root, 0);
+  traverse_fast_from<ANY, OCT, CLIP>(P, r, active, h, found, lds_stack, P.root, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1489,7 +1596,23 @@ __device__ __forceinline__ void trace(const DevScene& P, const Ray& r, bool acti
 // octants is walked once per octant present, each walk with that octant's lanes only (ballot masks) and
 // the octant loop's cheaper slab test, instead of one generic walk of the union; a one-octant packet is
 // the loop's single iteration. Each lane is traced by exactly one walk, so results are unchanged.
-template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false, bool WIDE = false, bool SPLIT = false>
+// Whether every active ray of the wave enters the root's box at t >= 0 or misses it (its origin is not
+// inside the scene's bounds and the scene is not behind it): then the octant loops may skip the entry
+// distance's clip at 0 (slab_o CLIP), two VALU per node step. Uniform.
+#ifndef RT_NOCLIP
+#define RT_NOCLIP 0
+#endif
+template <int OCT>
+__device__ __forceinline__ bool packet_in_front(const DevScene& P, const Ray& r, bool active) {
+  if (is_leaf(P.root)) return false;
+  const Node64 rn = sload_node(P.nodes, P.root);
+  const float lx = fminf(rn.c0lx, rn.c1lx), ly = fminf(rn.c0ly, rn.c1ly), lz = fminf(rn.c0lz, rn.c1lz);
+  const float hx = fmaxf(rn.c0hx, rn.c1hx), hy = fmaxf(rn.c0hy, rn.c1hy), hz = fmaxf(rn.c0hz, rn.c1hz);
+  const Span s = slab_o<OCT, false>(lx, hx, ly, hy, lz, hz, r, INFINITY);
+  return ballot(active && !(s.tmin >= 0.0f || s.tmin > s.tmax)) == 0;
+}
+template <bool ANY, bool STATS, int TRAV, bool LANE_MIXED = false, bool WIDE = false, bool SPLIT = false,
+          bool NOCLIP = false>
 __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                           WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   if (SPLIT && RT_OCT_SPECIALIZE && RT_FAST_LOOP && !STATS && TRAV == TRAV_B2_LDS) {
@@ -1545,6 +1668,18 @@ __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool 
         }
 #undef RT_WIDE_CASE
       }
+      if (NOCLIP && RT_NOCLIP && RT_FAST_LOOP && !STATS && SL) {
+#define RT_NOCLIP_CASE(o)                                                                      \
+  case o:                                                                                     \
+    if (packet_in_front<o>(P, r, active)) traverse_fast<ANY, o, false>(P, r, active, h, found, L.stack[wv]); \
+    else traverse_fast<ANY, o>(P, r, active, h, found, L.stack[wv]);                          \
+    return;
+        switch (oct) {
+          RT_NOCLIP_CASE(0) RT_NOCLIP_CASE(1) RT_NOCLIP_CASE(2) RT_NOCLIP_CASE(3)
+          RT_NOCLIP_CASE(4) RT_NOCLIP_CASE(5) RT_NOCLIP_CASE(6) default: RT_NOCLIP_CASE(7)
+        }
+#undef RT_NOCLIP_CASE
+      }
       if (RT_FAST_LOOP && !STATS && SL) {
         switch (oct) {
           case 0: traverse_fast<ANY, 0>(P, r, active, h, found, L.stack[wv]); return;
@@ -1576,11 +1711,11 @@ __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool 
   }
   trace<ANY, STATS, TRAV>(P, r, active, h, found, L, wv, cnt);
 }
-template <bool STATS, int TRAV, bool WIDE = false>
+template <bool STATS, int TRAV, bool WIDE = false, bool NOCLIP = false>
 __device__ __forceinline__ void trace_closest_oct(const DevScene& P, const Ray& r, bool active, Hit& h,
                                                   WaveLds<TRAV, STATS>& L, int wv, uint32_t* cnt) {
   bool found = false;
-  trace_oct<false, STATS, TRAV, false, WIDE>(P, r, active, h, found, L, wv, cnt);
+  trace_oct<false, STATS, TRAV, false, WIDE, false, NOCLIP>(P, r, active, h, found, L, wv, cnt);
 }
 
 // FULL mode: primary, reflection and shadow packets also take the octant-specialised loops when the
@@ -2213,8 +2348,15 @@ void k_primary_fused(FrameParams P) {
   const Ray r = primary_ray(P, c.px, c.py);
 #endif
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  trace_closest_oct<false, TRAV_B2_LDS, true>(P.sc, r, c.active, h, lds, c.slot, nullptr);
+  trace_closest_oct<false, TRAV_B2_LDS, true, true>(P.sc, r, c.active, h, lds, c.slot, nullptr);
+#if defined(RT_EXP_NOSHADE)  // timing experiment only: the hit distance instead of the shading
+  if (c.active) {
+    const size_t pix = (size_t)c.py * P.W + c.px;
+    P.rgb[3 * pix] = h.t; P.rgb[3 * pix + 1] = __uint_as_float(h.slot); P.rgb[3 * pix + 2] = 0.0f;
+  }
+#else
   if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
+#endif
   wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
 }
 
