@@ -175,7 +175,11 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 // that wanted the entry still could (every such lane's entry distance into it, recorded at the push,
 // now beyond its closest hit) -- what culling at the pop would save (rt_debug_counters)
 // ST_WWIDE: 128-B fp32 4-wide node records fetched per wave (ST_WNODE: 64-B binary / quantised records)
-enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_WWIDE, ST_COUNT };
+// ST_WCAND / ST_WPRE / ST_WINS (counting run, per wave-level triangle test): some lane passed the plane-
+// distance stage; some candidate lane's hit point lies inside the triangle's bounding box grown by 1e-3 of
+// its extent (what a box prefilter would keep); some lane passed the reference's edge tests
+enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_WWIDE,
+       ST_WCAND, ST_WPRE, ST_WINS, ST_COUNT };
 constexpr int kStatSlots = 16;
 
 struct Hit {
@@ -326,12 +330,12 @@ __device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_in
 
 // Rare path of a candidate (uniform triangle): interpolated normal non-zero (calculateDistance's
 // norm()==0 check, flyscene.cpp:467) and the reference box predicate. All loads wave-uniform.
-__device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0,
-                                                    f3 a1, f3 a2, f3 p, const Ray& r, uint64_t cand) {
+__device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const TriRec64& tr, uint32_t slot, f3 e0, f3 e2,
+                                                    f3 a0, f3 a1, f3 a2, f3 p, const Ray& r, uint64_t cand) {
   if (!(tr.box & kSafeNormalBit)) {  // uniform branch: only faces the host could not certify
     const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
     const float area = norm(cross(e0, neg(e2))) / 2;
-    const float* fs = P.fshade + 12 * (size_t)tr.face;
+    const float* fs = P.fshade + 12 * (size_t)slot;
     const f3 n0 = ld3(fs), n1 = ld3(fs + 4), n2 = ld3(fs + 8);
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
     cand &= fmask<kFcmpUNE>(norm(nn), 0.0f);
@@ -360,9 +364,9 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
 #ifndef RT_TRI_CLASS  // 1: the closest-hit candidate range test as one v_cmp_class (same set)
 #define RT_TRI_CLASS 1
 #endif
-template <bool ANY>
+template <bool ANY, bool STATS = false>
 __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, uint32_t slot, const Ray& r,
-                                         uint64_t act, Hit& h, bool& found) {
+                                         uint64_t act, Hit& h, bool& found, uint32_t* cnt = nullptr) {
   const f3 n{tr.nx, tr.ny, tr.nz};
   const float dn = dot(n, r.d);                 // facenormal.dot(dir)
   const float orth = tr.dist - dot(r.o, n);     // distancePlane - origin.dot(facenormal)
@@ -381,9 +385,18 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
       cand &= fmask<kFcmpOLT>(t, INFINITY) &
               (fmask<kFcmpOLT>(t, h.t) | (fmask<kFcmpOEQ>(t, h.t) & __builtin_amdgcn_uicmp(tr.rank, h.rank, kIcmpULT)));
   }
+  if (STATS) cnt[ST_WCAND] += cand != 0;
   if (cand == 0) return;
   const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
+  if (STATS) {
+    const f3 lo{fminf(fminf(w0.x, w1.x), w2.x), fminf(fminf(w0.y, w1.y), w2.y), fminf(fminf(w0.z, w1.z), w2.z)};
+    const f3 hi{fmaxf(fmaxf(w0.x, w1.x), w2.x), fmaxf(fmaxf(w0.y, w1.y), w2.y), fmaxf(fmaxf(w0.z, w1.z), w2.z)};
+    const float m = 1e-3f * fmaxf(fmaxf(hi.x - lo.x, hi.y - lo.y), hi.z - lo.z);
+    const bool in = p.x >= lo.x - m && p.x <= hi.x + m && p.y >= lo.y - m && p.y <= hi.y + m &&
+                    p.z >= lo.z - m && p.z <= hi.z + m;
+    cnt[ST_WPRE] += (cand & ballot(in)) != 0;
+  }
 #if RT_TRI_VREG
   // the record is wave-uniform (SGPRs) and a VALU op reads at most one SGPR: w0 and w1 copied into
   // VGPRs once serve all three edge differences (6 moves instead of 9; same float operations)
@@ -395,8 +408,9 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
 #endif
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
   cand &= ~ballot((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0));
+  if (STATS) cnt[ST_WINS] += cand != 0;
   if (cand == 0) return;
-  const bool acc = lane_in(accept_candidate(P, tr, e0, e2, a0, a1, a2, p, r, cand));
+  const bool acc = lane_in(accept_candidate(P, tr, slot, e0, e2, a0, a1, a2, p, r, cand));
   if (ANY) {
     found = found | acc;
   } else {
@@ -555,7 +569,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       }
       for (uint32_t k = 0; k < count; k++) {
         const TriRec64 tr = sload_tri(P.tris, first + k);
-        test_tri<ANY>(P, tr, first + k, r, act, h, found);
+        test_tri<ANY, STATS>(P, tr, first + k, r, act, h, found, cnt);
       }
 #ifdef RT_EXPERIMENT_TRIS_TWICE  // timing experiment only: the same leaf tested again (no effect)
       for (uint32_t k = 0; k < count; k++) {
@@ -633,9 +647,16 @@ __device__ __forceinline__ uint32_t lds_pop_at(const uint32_t* stack, uint32_t s
 
 // traverse_fast from a given state (node handle, stack depth): the whole traversal starts at the root
 // with an empty stack; the dual-chain loop (traverse_dual) hands over a half-finished one
-template <bool ANY, int OCT, bool CLIP = true>
+// VST: the wave stack lives in the 64 lanes of one VGPR (v_writelane push, v_readlane pop: one VALU op
+// each, no LDS address moves and no LDS read latency on the pop) -- only for a caller whose exec mask is
+// full throughout (k_primary_fused): a VGPR copy under a partial exec mask would drop stack entries
+#ifndef RT_VSTACK
+#define RT_VSTACK 0
+#endif
+template <bool ANY, int OCT, bool CLIP = true, bool VST = false>
 __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                                    uint32_t* lds_stack, uint32_t node, int sp) {
+  int vstk = 0;  // VST: lane k holds stack entry k
   uint64_t act = ballot(active);  // lanes still tracing: used by the triangle tests only
   float tlim = active ? INFINITY : -1.0f;  // ANY: box-test limit (-1 once the lane is blocked)
   if (!ANY && !active) h.t = -1.0f;
@@ -687,7 +708,8 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
             : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [c0] "s"(uniform(nd.child0)),
               [c1] "s"(uniform(nd.child1))
             : "scc");
-        if (RT_STACK_ASM) lds_push_at(lds_stack, (uint32_t)sp, farb);
+        if (VST) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(vstk) : "s"(farb), "s"(sp));
+        else if (RT_STACK_ASM) lds_push_at(lds_stack, (uint32_t)sp, farb);
         else lds_push(lds_stack + sp, farb);
       }
       if ((RT_PF_MODE == 4 || RT_PF_MODE == 5) && RT_EARLY_PUSH && RT_ORDER_BITS && OCT >= 0) {
@@ -919,7 +941,8 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
       node = uniform(tos);
       tos = lds_stack[sp > 0 ? sp - 1 : 0];
     } else {
-      node = RT_STACK_ASM ? lds_pop_at(lds_stack, (uint32_t)sp) : uniform(lds_stack[sp]);
+      node = VST ? (uint32_t)__builtin_amdgcn_readlane(vstk, sp)
+                 : RT_STACK_ASM ? lds_pop_at(lds_stack, (uint32_t)sp) : uniform(lds_stack[sp]);
     }
   }
 #if RT_PREFETCH && RT_PF_CARRY
@@ -930,11 +953,11 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
   if (!ANY && !active) h.t = INFINITY;
 }
 
-template <bool ANY, int OCT, bool CLIP = true>
+template <bool ANY, int OCT, bool CLIP = true, bool VST = false>
 __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                               uint32_t* lds_stack) {
   if (P.n_nodes == 0) return;
-  traverse_fast_from<ANY, OCT, CLIP>(P, r, active, h, found, lds_stack, P.root, 0);
+  traverse_fast_from<ANY, OCT, CLIP, VST>(P, r, active, h, found, lds_stack, P.root, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1467,12 +1490,12 @@ __device__ __forceinline__ T vload64(const T* base, uint32_t i) {
 }
 
 // the rare accept path of one lane (accept_candidate, per lane)
-__device__ __forceinline__ bool accept_lane(const DevScene& P, const TriRec64& tr, f3 e0, f3 e2, f3 a0, f3 a1, f3 a2,
-                                            f3 p, const Ray& r) {
+__device__ __forceinline__ bool accept_lane(const DevScene& P, const TriRec64& tr, uint32_t slot, f3 e0, f3 e2, f3 a0,
+                                            f3 a1, f3 a2, f3 p, const Ray& r) {
   if (!(tr.box & kSafeNormalBit)) {
     const float area0 = norm(a0) / 2, area1 = norm(a1) / 2, area2 = norm(a2) / 2;
     const float area = norm(cross(e0, neg(e2))) / 2;
-    const float* fs = P.fshade + 12 * (size_t)tr.face;
+    const float* fs = P.fshade + 12 * (size_t)slot;
     const f3 n0 = ld3(fs), n1 = ld3(fs + 4), n2 = ld3(fs + 8);
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
     if (!(norm(nn) != 0)) return false;
@@ -1506,7 +1529,7 @@ __device__ __forceinline__ void test_tri_lane(const DevScene& P, const TriRec64&
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
   if ((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0)) return;
-  if (!accept_lane(P, tr, e0, e2, a0, a1, a2, p, r)) return;
+  if (!accept_lane(P, tr, slot, e0, e2, a0, a1, a2, p, r)) return;
   if (ANY) {
     found = true;
   } else {
@@ -1671,8 +1694,8 @@ __device__ __forceinline__ void trace_oct(const DevScene& P, const Ray& r, bool 
       if (NOCLIP && RT_NOCLIP && RT_FAST_LOOP && !STATS && SL) {
 #define RT_NOCLIP_CASE(o)                                                                      \
   case o:                                                                                     \
-    if (packet_in_front<o>(P, r, active)) traverse_fast<ANY, o, false>(P, r, active, h, found, L.stack[wv]); \
-    else traverse_fast<ANY, o>(P, r, active, h, found, L.stack[wv]);                          \
+    if (packet_in_front<o>(P, r, active)) traverse_fast<ANY, o, false, RT_VSTACK>(P, r, active, h, found, L.stack[wv]); \
+    else traverse_fast<ANY, o, true, RT_VSTACK>(P, r, active, h, found, L.stack[wv]);                  \
     return;
         switch (oct) {
           RT_NOCLIP_CASE(0) RT_NOCLIP_CASE(1) RT_NOCLIP_CASE(2) RT_NOCLIP_CASE(3)
@@ -1771,12 +1794,14 @@ __device__ __forceinline__ MatState load_mat(const DevMat& m) {
 
 // interpolateNormal (flyscene.cpp:572-600) for the hit triangle of this lane: one contiguous 48-B
 // gather of the face's shading record (its three unit vertex normals + material)
-__device__ __forceinline__ f3 hit_normal(const DevScene& P, const TriRec64& tr, f3 p, int32_t& mat) {
+// the shading record is indexed by the triangle slot (like the record itself), so its gather does not wait
+// for the record's face id: both loads of a hit are issued together
+__device__ __forceinline__ f3 hit_normal(const DevScene& P, const TriRec64& tr, uint32_t slot, f3 p, int32_t& mat) {
   const f3 n{tr.nx, tr.ny, tr.nz};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
   const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  const float4* fs = reinterpret_cast<const float4*>(P.fshade + 12 * (size_t)tr.face);
+  const float4* fs = reinterpret_cast<const float4*>(P.fshade + 12 * (size_t)slot);
   const float4 n0 = fs[0];
   mat = __float_as_int(n0.w);
   if (dot(n, a0) < 0 || dot(n, a1) < 0 || dot(n, a2) < 0) return f3{0.0f, 0.0f, 0.0f};
@@ -2024,7 +2049,9 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
 #pragma unroll
   for (int c = 0; c < ST_COUNT; c++) {
     unsigned long long v = cnt[c];
-    if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL || c == ST_WWIDE) v = (lane == 0) ? v : 0;  // wave counts once
+    if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL || c == ST_WWIDE || c == ST_WCAND || c == ST_WPRE ||
+        c == ST_WINS)
+      v = (lane == 0) ? v : 0;  // wave counts once
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(P.stats + c, v);
   }
@@ -2260,7 +2287,7 @@ __device__ __forceinline__ void shade_primary_pixel(const FrameParams& P, const 
     hi0.face = tr0.face;
     face = (int32_t)tr0.face;
     hi0.p = f3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
-    hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
+    hi0.n = hit_normal(P.sc, tr0, slot, hi0.p, hi0.mat);
     MatState st = load_mat(P.defmat);
     const f3 direct0 = calc_color<false, false, TRAV_B2_LDS>(P, st, hi0, r.o, true, nullptr, 0, nullptr);
     if (hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;
@@ -2434,7 +2461,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
     const TriRec64 tr0 = vload_tri(P.sc.tris, h.slot);
     hi0.face = tr0.face;
     hi0.p = f3{r.o.x + h.t * r.d.x, r.o.y + h.t * r.d.y, r.o.z + h.t * r.d.z};
-    hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
+    hi0.n = hit_normal(P.sc, tr0, h.slot, hi0.p, hi0.mat);
   }
   // the primary hits' shadow packets head for the same light from neighbouring points: octant loops for
   // them too (A/B knob RT_FULL_OCT_SHADOW); the reflection hits' shadows keep the generic loop
@@ -2463,7 +2490,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
     const TriRec64 tr1 = vload_tri(P.sc.tris, h1.slot);
     hi1.face = tr1.face;
     hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
-    hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
+    hi1.n = hit_normal(P.sc, tr1, h1.slot, hi1.p, hi1.mat);
   }
   const f3 direct1 = calc_color<true, STATS, TRAV, RT_FULL_OCT_SHADOW2 != 0, SPLIT>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
   if (hit1) {
@@ -2513,7 +2540,7 @@ __device__ __forceinline__ f3 trace_full_loop(const FrameParams& P, const Ray& r
       const TriRec64 tr = vload_tri(P.sc.tris, h.slot);
       hi.face = tr.face;
       hi.p = f3{cur.o.x + h.t * cur.d.x, cur.o.y + h.t * cur.d.y, cur.o.z + h.t * cur.d.z};
-      hi.n = hit_normal(P.sc, tr, hi.p, hi.mat);
+      hi.n = hit_normal(P.sc, tr, h.slot, hi.p, hi.mat);
     }
     const f3 direct = calc_color<true, STATS, TRAV>(P, st, hi, cur.o, hit, &lds, wv, cnt);
     if (depth == 0) {
@@ -2637,7 +2664,7 @@ void k_render_depth(FrameParams P) {
       const TriRec64 tr = vload_tri(P.sc.tris, h.slot);
       hi.face = tr.face;
       hi.p = f3{cur.o.x + h.t * cur.d.x, cur.o.y + h.t * cur.d.y, cur.o.z + h.t * cur.d.z};
-      hi.n = hit_normal(P.sc, tr, hi.p, hi.mat);
+      hi.n = hit_normal(P.sc, tr, h.slot, hi.p, hi.mat);
     }
     if (d == 0) {
       h0 = h;
@@ -2786,7 +2813,7 @@ __global__ __launch_bounds__(256) void k_full_gen0(FrameParams P) {
     HitInfo hi0;
     hi0.face = tr0.face;
     hi0.p = f3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
-    hi0.n = hit_normal(P.sc, tr0, hi0.p, hi0.mat);
+    hi0.n = hit_normal(P.sc, tr0, hb.y, hi0.p, hi0.mat);
     hs = to_state(hi0);
     const f3 d = reflect(normalized(r.d), hi0.n);
     const f3 o = offset(hi0.p, d, 0.001f);
@@ -2877,7 +2904,7 @@ __global__ __launch_bounds__(256) void k_full_gen1(FrameParams P) {
     HitInfo hi1;
     hi1.face = tr1.face;
     hi1.p = f3{rq.ox + t * rq.dx, rq.oy + t * rq.dy, rq.oz + t * rq.dz};
-    hi1.n = hit_normal(P.sc, tr1, hi1.p, hi1.mat);
+    hi1.n = hit_normal(P.sc, tr1, hb.y, hi1.p, hi1.mat);
     hs = to_state(hi1);
   }
   P.state1[pix] = hs;
@@ -2980,7 +3007,7 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
     }
     if (R.N) {  // interpolateNormal(face, P) (flyscene.cpp:572-600)
       int32_t mat;
-      const f3 nn = hit_normal(P.sc, tr, p, mat);
+      const f3 nn = hit_normal(P.sc, tr, h.slot, p, mat);
       R.N[3 * (size_t)i + 0] = nn.x;
       R.N[3 * (size_t)i + 1] = nn.y;
       R.N[3 * (size_t)i + 2] = nn.z;
@@ -3198,11 +3225,14 @@ int device_upload(rt_scene* s) {
   }
   if ((rc = dalloc_copy(&s->d_nodes4, hs.nodes4.data(), hs.nodes4.size() * sizeof(Node4Q), tot))) return rc;
   {
-    // per-face shading record (float4 x 3): the unit normals of the face's three vertices (Mesh normals
-    // as interpolateNormal normalises them, flyscene.cpp:599) and the material id in the first .w
-    std::vector<float> fsh(12 * (size_t)hs.nf, 0.0f);
-    for (int32_t f = 0; f < hs.nf; f++) {
-      float* r = fsh.data() + 12 * (size_t)f;
+    // per-slot shading record (float4 x 3), in the triangle records' (BVH leaf) order: the unit normals of
+    // the slot's face's three vertices (Mesh normals as interpolateNormal normalises them,
+    // flyscene.cpp:599) and the material id in the first .w. Indexed by slot, not face id, so a hit's two
+    // gathers (triangle record, shading record) are independent and issue together.
+    std::vector<float> fsh(12 * hs.tris.size(), 0.0f);
+    for (size_t sl = 0; sl < hs.tris.size(); sl++) {
+      const uint32_t f = hs.tris[sl].face;
+      float* r = fsh.data() + 12 * sl;
       for (int k = 0; k < 3; k++) {
         const f3 n = hs.vnn[hs.fidx[3 * f + k]];
         r[4 * k] = n.x; r[4 * k + 1] = n.y; r[4 * k + 2] = n.z;

@@ -5,7 +5,7 @@
 //                                  (one 64-B record = one s_load_dwordx16 per wave per visit)
 //   tris     TriRec64[n_faces]     exact-test data in BVH leaf order: unit face normal, plane distance,
 //                                  world vertices, reference rank / face id / reference box id
-//   fshade   float4[3*n_faces]     per face id: the three normalised vertex normals (interpolateNormal,
+//   fshade   float4[3*n_slots]     per triangle slot (BVH leaf order): the three normalised vertex normals (interpolateNormal,
 //                                  flyscene.cpp:599) + material id; read by the final hit (one 48-B gather)
 //   refbox   float4[2*n_boxes]     reference flat boxes, object space (BoundingBox::low/high)
 //   mats     float4[3*n_mats]      ka|Ns, kd|-, ks|- per material
@@ -136,7 +136,7 @@ struct DevScene {
   uint32_t wide_base, wide_copy_bytes;
   float static_pad;        // the pad every BVH box carries (setup_cull adds a ray's own pad beyond it)
   const TriRec64* tris;
-  const float* fshade;     // float4 x 3 per face: unit vertex normals (n0 .w = material id bits)
+  const float* fshade;     // float4 x 3 per triangle slot: unit vertex normals (n0 .w = material id bits)
   const float* refbox;     // 2 float4 per box
   const DevMat* mats;
   uint32_t root;           // root handle; n_nodes == 0 -> empty scene

@@ -1,4 +1,4 @@
-"""Counting run of the C3 soup / bunny frames (RT_FRAME_STATS) and the raw counters of rt_debug_counters:
+"""Counting run (also the wave-level triangle-stage counts) of the C3 soup / bunny frames (RT_FRAME_STATS) and the raw counters of rt_debug_counters:
 how many wave stack pops there are per wave, and how many of them no lane still needed (every lane that
 had wanted the entry now has a closest hit nearer than its entry distance) -- the node steps that a
 culling test at the pop would save. Usage: python tools/pop_stats.py [soup|bunny ...]"""
@@ -12,7 +12,8 @@ import conftest  # noqa: E402
 
 rt = conftest.rtamd
 NAMES = ["node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "primary_rays", "hits",
-         "total_rays", "wave_pops", "wave_pops_cullable"]
+         "total_rays", "wave_pops", "wave_pops_cullable", "wave_wide_fetches", "wave_tri_cand", "wave_tri_prebox",
+         "wave_tri_inside"]
 
 
 def main(scenes):
@@ -32,6 +33,11 @@ def main(scenes):
         d["pops_per_wave"] = d["wave_pops"] / waves
         d["node_steps_per_wave"] = d["wave_node_fetches"] / waves
         d["cullable_share_of_pops"] = d["wave_pops_cullable"] / max(d["wave_pops"], 1)
+        wt = max(d["wave_tri_fetches"], 1)
+        d["tri_tests_per_wave"] = d["wave_tri_fetches"] / waves
+        d["tri_share_cand"] = d["wave_tri_cand"] / wt  # some lane past the plane-distance stage
+        d["tri_share_prebox"] = d["wave_tri_prebox"] / wt  # some candidate's hit point in the grown triangle box
+        d["tri_share_inside"] = d["wave_tri_inside"] / wt  # some lane past the edge tests
         print(json.dumps(d), flush=True)
 
 
