@@ -177,9 +177,10 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 // ST_WWIDE: 128-B fp32 4-wide node records fetched per wave (ST_WNODE: 64-B binary / quantised records)
 // ST_WCAND / ST_WPRE / ST_WINS (counting run, per wave-level triangle test): some lane passed the plane-
 // distance stage; some candidate lane's hit point lies inside the triangle's bounding box grown by 1e-3 of
-// its extent (what a box prefilter would keep); some lane passed the reference's edge tests
+// its extent (what a box prefilter would keep); some lane passed the reference's edge tests. ST_WE1 / ST_WE2:
+// the staged edge tests (RT_TRI_STAGED) left no candidate after the first / the second edge
 enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_WWIDE,
-       ST_WCAND, ST_WPRE, ST_WINS, ST_COUNT };
+       ST_WCAND, ST_WPRE, ST_WINS, ST_WE1, ST_WE2, ST_COUNT };
 constexpr int kStatSlots = 16;
 
 struct Hit {
@@ -361,6 +362,9 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
 // calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record, for the lanes of
 // `act`. CLOSEST: update (t, rank, slot) if 0 <= t < best (rank breaks ties as the reference's order
 // does). ANY: any valid t >= 0 (shadow(), flyscene.cpp:519).
+#ifndef RT_TRI_STAGED  // 1: the three edge tests one at a time, the wave leaving once no candidate is left
+#define RT_TRI_STAGED 1
+#endif
 #ifndef RT_TRI_CLASS  // 1: the closest-hit candidate range test as one v_cmp_class (same set)
 #define RT_TRI_CLASS 1
 #endif
@@ -406,8 +410,25 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
 #else
   const f3 e0 = sub(w1, w0), e1 = sub(w2, w1), e2 = sub(w0, w2);
 #endif
-  const f3 a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
-  cand &= ~ballot((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0));
+  f3 a0, a1, a2;
+  if (RT_TRI_STAGED || STATS) {
+    // the reference's three edge tests are independent (interpolateNormal, flyscene.cpp:591: rejected if any is
+    // negative), so they run one at a time and the wave stops as soon as no candidate lane is left --
+    // the same values, the same set; a packet wholly beyond one edge line skips the other edges' work
+    a0 = cross(e0, sub(p, w0));
+    cand &= ~ballot(dot(n, a0) < 0);
+    if (STATS) cnt[ST_WE1] += cand == 0;
+    if (cand == 0) return;
+    a1 = cross(e1, sub(p, w1));
+    cand &= ~ballot(dot(n, a1) < 0);
+    if (STATS) cnt[ST_WE2] += cand == 0;
+    if (cand == 0) return;
+    a2 = cross(e2, sub(p, w2));
+    cand &= ~ballot(dot(n, a2) < 0);
+  } else {
+    a0 = cross(e0, sub(p, w0)), a1 = cross(e1, sub(p, w1)), a2 = cross(e2, sub(p, w2));
+    cand &= ~ballot((int)(dot(n, a0) < 0) | (int)(dot(n, a1) < 0) | (int)(dot(n, a2) < 0));
+  }
   if (STATS) cnt[ST_WINS] += cand != 0;
   if (cand == 0) return;
   const bool acc = lane_in(accept_candidate(P, tr, slot, e0, e2, a0, a1, a2, p, r, cand));
@@ -657,7 +678,9 @@ template <bool ANY, int OCT, bool CLIP = true, bool VST = false>
 __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                                    uint32_t* lds_stack, uint32_t node, int sp) {
   int vstk = 0;  // VST: lane k holds stack entry k
-  uint64_t act = ballot(active);  // lanes still tracing: used by the triangle tests only
+  // lanes still tracing: used by the any-hit triangle tests only (a closest-hit lane without a ray
+  // carries t_best = -1, which no candidate t >= -0 passes, so its triangle tests need no mask)
+  uint64_t act = ANY ? ballot(active) : ~0ull;
   float tlim = active ? INFINITY : -1.0f;  // ANY: box-test limit (-1 once the lane is blocked)
   if (!ANY && !active) h.t = -1.0f;
 #if RT_PREFETCH && RT_PF_CARRY
@@ -2050,7 +2073,7 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
   for (int c = 0; c < ST_COUNT; c++) {
     unsigned long long v = cnt[c];
     if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL || c == ST_WWIDE || c == ST_WCAND || c == ST_WPRE ||
-        c == ST_WINS)
+        c == ST_WINS || c == ST_WE1 || c == ST_WE2)
       v = (lane == 0) ? v : 0;  // wave counts once
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(P.stats + c, v);

@@ -13,7 +13,7 @@ import conftest  # noqa: E402
 rt = conftest.rtamd
 NAMES = ["node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "primary_rays", "hits",
          "total_rays", "wave_pops", "wave_pops_cullable", "wave_wide_fetches", "wave_tri_cand", "wave_tri_prebox",
-         "wave_tri_inside"]
+         "wave_tri_inside", "wave_tri_exit_edge1", "wave_tri_exit_edge2"]
 
 
 def main(scenes):
@@ -38,6 +38,8 @@ def main(scenes):
         d["tri_share_cand"] = d["wave_tri_cand"] / wt  # some lane past the plane-distance stage
         d["tri_share_prebox"] = d["wave_tri_prebox"] / wt  # some candidate's hit point in the grown triangle box
         d["tri_share_inside"] = d["wave_tri_inside"] / wt  # some lane past the edge tests
+        d["tri_share_exit_edge1"] = d["wave_tri_exit_edge1"] / wt  # staged edge tests: none left after edge 1
+        d["tri_share_exit_edge2"] = d["wave_tri_exit_edge2"] / wt
         print(json.dumps(d), flush=True)
 
 
