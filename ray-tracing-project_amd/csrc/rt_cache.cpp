@@ -227,7 +227,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
     if (hs.fmat[f] < -1 || hs.fmat[f] >= h.n_mats) { rt::set_error("rt_scene_load: bad material id"); return RT_ERR_IO; }
   }
   for (const rt::TriRec64& t : hs.tris)
-    if (t.face >= (uint32_t)h.nf || (t.box & ~rt::kSafeNormalBit) >= (uint32_t)h.n_boxes) {
+    if (t.face >= (uint32_t)h.nf || (t.box & rt::kBoxIndexMask) >= (uint32_t)h.n_boxes) {
       rt::set_error("rt_scene_load: bad triangle record");
       return RT_ERR_IO;
     }

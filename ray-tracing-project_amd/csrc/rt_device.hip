@@ -329,6 +329,9 @@ template <int PRED>
 __device__ __forceinline__ uint64_t fmask(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, PRED); }
 __device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
+#ifndef RT_BOX_CERT  // 1: certified faces (kBoxCertBit) skip the reference box predicate
+#define RT_BOX_CERT 1
+#endif
 // Rare path of a candidate (uniform triangle): interpolated normal non-zero (calculateDistance's
 // norm()==0 check, flyscene.cpp:467) and the reference box predicate. All loads wave-uniform.
 __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const TriRec64& tr, uint32_t slot, f3 e0, f3 e2,
@@ -341,10 +344,19 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
     cand &= fmask<kFcmpUNE>(norm(nn), 0.0f);
   }
+#if defined(RT_EXP_NO_BOXPRED)  // timing experiment only: the reference box predicate skipped (wrong results)
+  return cand;
+#endif
+  if (RT_BOX_CERT && (tr.box & kBoxCertBit)) {
+    // certified face (kBoxCertBit): the predicate holds for every candidate lane whose object-space
+    // origin is within the certified range (NaN fails the compare and takes the path below)
+    const float om = fmaxf(fmaxf(fabsf(r.o2.x), fabsf(r.o2.y)), fabsf(r.o2.z));
+    if ((cand & ~ballot(om <= P.cert_origin_max)) == 0) return cand;
+  }
   // reference box predicate. Fast path: the object-space hit point lies inside the reference box
   // with a margin (1e-5 relative) far above the reference slab test's rounding, so the exact ray
   // crosses the box interior at t >= 0 and intersectBox accepts. Otherwise run the exact test.
-  const float* bx = P.refbox + 8 * (size_t)(tr.box & ~kSafeNormalBit);
+  const float* bx = P.refbox + 8 * (size_t)(tr.box & kBoxIndexMask);
   const f3 X = affv3(P.Minv, p);
   const float lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[4], bx[5], bx[6]};
   const float xs[3] = {X.x, X.y, X.z}, os[3] = {r.o2.x, r.o2.y, r.o2.z};
@@ -1523,7 +1535,10 @@ __device__ __forceinline__ bool accept_lane(const DevScene& P, const TriRec64& t
     const f3 nn = blend_normal(n0, n1, n2, area0, area1, area2, area);
     if (!(norm(nn) != 0)) return false;
   }
-  const float* bx = P.refbox + 8 * (size_t)(tr.box & ~kSafeNormalBit);
+  if (RT_BOX_CERT && (tr.box & kBoxCertBit) &&
+      fmaxf(fmaxf(fabsf(r.o2.x), fabsf(r.o2.y)), fabsf(r.o2.z)) <= P.cert_origin_max)
+    return true;
+  const float* bx = P.refbox + 8 * (size_t)(tr.box & kBoxIndexMask);
   const f3 X = affv3(P.Minv, p);
   const float lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[4], bx[5], bx[6]};
   const float xs[3] = {X.x, X.y, X.z}, os[3] = {r.o2.x, r.o2.y, r.o2.z};
@@ -3176,6 +3191,7 @@ int device_upload(rt_scene* s) {
   tot = 0;
   int rc;
   s->static_pad = scene_static_pad(hs);
+  s->cert_origin_max = cert_origin_max(hs);
   {
     // BVH nodes and triangle records share one allocation (triangles right after the nodes), so one
     // base plus a 32-bit byte offset reaches either: with RT_PREFETCH each uploaded node's pad0 / pad1
@@ -3356,6 +3372,7 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.root4 = 0;
   P.sc.n_nodes4 = (int32_t)hs.nodes4.size();
   P.sc.static_pad = s->static_pad;
+  P.sc.cert_origin_max = s->cert_origin_max;
   P.sc.wide_base = s->wide_base;
   P.sc.wide_copy_bytes = s->wide_copy_bytes;
   memcpy(P.sc.Minv, hs.Minv, 64);

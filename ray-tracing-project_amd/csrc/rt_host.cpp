@@ -1268,8 +1268,62 @@ void world_bounds(const HostScene& hs, float lo[3], float hi[3]) {
   for (int k = 0; k < 3; k++) { lo[k] = w.lo[k]; hi[k] = w.hi[k]; }
 }
 
+// Reference-box certificates (TriRec64::box kBoxCertBit). The accept path's box fast path (rt_device.hip
+// accept_candidate) accepts a candidate lane whose object-space hit point X = Minv p lies inside the
+// face's reference box by m_k = 1e-5 ((hi - lo) + |lo| + |hi| + |o2_k|) per axis, o2 the ray's
+// object-space origin -- margins far above the rounding of the reference's intersectBox
+// (flyscene.cpp:484-507), so the reference accepts too. A face is certified when that fast path must
+// succeed for every hit point its edge tests can accept, for any ray whose |o2|_inf <= Ro =
+// cert_origin_max: its three object-space vertices lie inside the box by m_k(Ro) + delta_k, where
+// delta_k = 1e-5 ((hi - lo) + |lo| + |hi|) + 4e-4 diam covers how far a hit point the reference's
+// inclusive float edge tests accept can lie outside the triangle (at most a few ulp of |p - w| over
+// sin(theta_min / 2), here <= 0.01 diam -- only triangles whose smallest angle has sin(theta/2) >= 0.01
+// are certified) and the rounding of M / Minv (a similarity) and of X. Uncertified faces and rays
+// beyond Ro take the fast path and, where it fails, the exact test, as before.
+float cert_origin_max(const HostScene& hs) {
+  float R = 0.0f;
+  for (float v : hs.ov3) R = std::max(R, std::fabs(v));  // NaN coordinates are skipped by max
+  return std::isfinite(R) ? 16.0f * R : 0.0f;
+}
+
+static bool box_certified(const HostScene& hs, uint32_t f, float Ro) {
+  if (!(Ro > 0.0f) || hs.ov3.empty()) return false;
+  const RefBox& b = hs.boxes[hs.face_box[f]];
+  double v[3][3];
+  for (int j = 0; j < 3; j++)
+    for (int k = 0; k < 3; k++) {
+      v[j][k] = hs.ov3[3 * (size_t)hs.fidx[3 * f + j] + k];
+      if (!std::isfinite(v[j][k])) return false;
+    }
+  // edge lengths and the smallest angle (law of cosines, in double)
+  double L[3];
+  for (int j = 0; j < 3; j++) {
+    const double* a = v[j];
+    const double* c = v[(j + 1) % 3];
+    L[j] = std::sqrt((c[0] - a[0]) * (c[0] - a[0]) + (c[1] - a[1]) * (c[1] - a[1]) + (c[2] - a[2]) * (c[2] - a[2]));
+  }
+  const double diam = std::max(L[0], std::max(L[1], L[2]));
+  if (!(diam > 0.0)) return false;
+  for (int j = 0; j < 3; j++) {  // angle opposite edge j: between edges j+1 and j+2
+    const double a = L[(j + 1) % 3], c = L[(j + 2) % 3], o = L[j];
+    if (!(a > 0.0 && c > 0.0)) return false;
+    const double cosv = std::min(1.0, std::max(-1.0, (a * a + c * c - o * o) / (2.0 * a * c)));
+    const double s_half = std::sqrt(std::max(0.0, (1.0 - cosv) / 2.0));  // sin(theta / 2)
+    if (!(s_half >= 0.01)) return false;
+  }
+  for (int k = 0; k < 3; k++) {
+    const double lo = b.low[k], hi = b.high[k];
+    if (!std::isfinite(lo) || !std::isfinite(hi)) return false;
+    const double S = (hi - lo) + std::fabs(lo) + std::fabs(hi);
+    const double need = 1e-5 * (S + Ro) + 1e-30 + 1e-5 * S + 4e-4 * diam;
+    for (int j = 0; j < 3; j++)
+      if (!(v[j][k] - lo >= need && hi - v[j][k] >= need)) return false;
+  }
+  return true;
+}
+
 // exact-test record of face f (the kernels' TriRec64)
-static void tri_record(const HostScene& hs, uint32_t f, TriRec64& r) {
+static void tri_record(const HostScene& hs, uint32_t f, TriRec64& r, float Ro) {
   const f3& n = hs.fnn[f];
   const f3& w0 = hs.wv[hs.fidx[3 * f]];
   const f3& w1 = hs.wv[hs.fidx[3 * f + 1]];
@@ -1280,13 +1334,14 @@ static void tri_record(const HostScene& hs, uint32_t f, TriRec64& r) {
   r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
   r.rank = hs.face_rank[f];
   r.face = f;
-  r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u);
+  r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u) | (box_certified(hs, f, Ro) ? kBoxCertBit : 0u);
 }
 
 void face_records(const HostScene& hs, std::vector<TriRec64>& out) {
   out.resize(hs.nf);
+  const float Ro = cert_origin_max(hs);
   parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int) {
-    for (size_t f = b; f < e; f++) tri_record(hs, (uint32_t)f, out[f]);
+    for (size_t f = b; f < e; f++) tri_record(hs, (uint32_t)f, out[f], Ro);
   });
 }
 
@@ -1442,13 +1497,17 @@ static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, c
   relayout_dfs(hs, tmp, root);
   hs.leaves = (int)B.nleaf.load();
   hs.tris.resize(order.size());
+  const float Ro = cert_origin_max(hs);
   parallel_chunks(order.size(), [&](size_t sb, size_t se, int) {
-    for (size_t i = sb; i < se; i++) tri_record(hs, order[i], hs.tris[i]);
+    for (size_t i = sb; i < se; i++) tri_record(hs, order[i], hs.tris[i], Ro);
   });
-  if (getenv("RT_TIMING"))
-    fprintf(stderr, "[rt] sbvh build %.1f ms: %zu references for %d faces, %u nodes\n",
+  if (getenv("RT_TIMING")) {
+    size_t cert = 0;
+    for (const TriRec64& t : hs.tris) cert += (t.box & kBoxCertBit) != 0;
+    fprintf(stderr, "[rt] sbvh build %.1f ms: %zu references for %d faces, %u nodes, %zu references box-certified\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count(), order.size(),
-            hs.nf, nn);
+            hs.nf, nn, cert);
+  }
 }
 
 void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
@@ -1506,8 +1565,9 @@ void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
   hs.leaves = B.leaves.load();
   // triangle records in leaf order
   hs.tris.resize(hs.nf);
+  const float Ro = cert_origin_max(hs);
   parallel_chunks((size_t)hs.nf, [&](size_t sb, size_t se, int) {
-    for (size_t s = sb; s < se; s++) tri_record(hs, prims[s].id, hs.tris[s]);
+    for (size_t s = sb; s < se; s++) tri_record(hs, prims[s].id, hs.tris[s], Ro);
   });
 }
 

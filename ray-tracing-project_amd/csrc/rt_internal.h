@@ -34,6 +34,12 @@ constexpr int kMaxDepth = 60;  // wave stack holds 64 entries; occupancy <= dept
 // TriRec64::box bit 31: the triangle's interpolated normal can never be the zero vector (see
 // rt_host.cpp safe_normal()), so calculateDistance's norm()==0 rejection never fires for it
 constexpr uint32_t kSafeNormalBit = 0x80000000u;
+// TriRec64::box bit 30: reference-box certificate (rt_host.cpp box_certified()): for a ray whose
+// object-space origin lies within DevScene::cert_origin_max (max norm), every hit point the reference's
+// edge tests accept on this face lies inside the face's reference box by more than the box fast path's
+// margin, so intersectBox accepts and the accept path skips the box predicate
+constexpr uint32_t kBoxCertBit = 0x40000000u;
+constexpr uint32_t kBoxIndexMask = 0x3FFFFFFFu;  // TriRec64::box without its flag bits
 
 RT_HD bool is_leaf(uint32_t h) { return (h & kLeafBit) != 0; }
 RT_HD uint32_t leaf_first(uint32_t h) { return h & kLeafFirstMask; }
@@ -110,7 +116,7 @@ struct alignas(16) TriRec64 {
   float w2z;
   uint32_t rank;  // position in the reference's (box, in-box) iteration order: tie-break key
   uint32_t face;  // original mesh face index
-  uint32_t box;   // reference box holding the face (intersectBox predicate) | kSafeNormalBit
+  uint32_t box;   // reference box holding the face (intersectBox predicate) | kSafeNormalBit | kBoxCertBit
 };
 static_assert(sizeof(TriRec64) == 64, "triangle record must be 64 bytes");
 
@@ -142,6 +148,7 @@ struct DevScene {
   uint32_t root;           // root handle; n_nodes == 0 -> empty scene
   int32_t n_nodes;
   float Minv[16];          // getShapeModelMatrix().inverse() (object-space hit point for the box fast path)
+  float cert_origin_max;   // kBoxCertBit holds for rays whose object-space origin has max norm <= this
 };
 
 // hit information handed between FULL stage kernels (32 B); face == 0xFFFFFFFF: no hit

@@ -72,6 +72,7 @@ void build_bvh4(HostScene& hs);
 void build_wide(HostScene& hs);
 float bvh_pad(const float lo[3], const float hi[3]);
 float scene_static_pad(const HostScene& hs);
+float cert_origin_max(const HostScene& hs);
 void set_error(const char* fmt, ...);
 
 }  // namespace rt
@@ -92,6 +93,7 @@ struct rt_scene {
   rt::TriRec64* d_tris = nullptr;
   uint32_t wide_base = 0, wide_copy_bytes = 0;  // fp32 4-wide tree in d_nodes (DevScene), 0: none
   float static_pad = 0.0f;  // the pad every BVH box carries (DevScene::static_pad)
+  float cert_origin_max = 0.0f;  // DevScene::cert_origin_max (cert_origin_max(hs))
   float* d_fshade = nullptr;  // per-face shading record: three unit vertex normals + material (float4 x 3)
   float* d_refbox = nullptr;
   // RT_MODE_BOX_COLORS: the boxes' colours and, per face id, the sum of the colours of the boxes that

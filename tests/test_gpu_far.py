@@ -5,7 +5,8 @@ fly camera can move anywhere (dependencies/tucano/tucano/utils/flycamera.hpp:196
 a BVH whose boxes carry a static, scene-scale pad plus a per-ray pad proportional to the ray origin's
 magnitude (setup_cull, rt_device.hip). These tests put the origin where the rounding
 of the reference's hit point P = o + t d is largest relative to the scene -- eyes at 50 and 500 scene
-extents (narrow fields of view, so the scene still fills the frame), a grazing view along a face plane,
+extents (narrow fields of view, so the scene still fills the frame), eyes at 3-7 extents (inside the range
+where certified faces skip the reference box predicate), a grazing view along a face plane,
 ray-list queries from up to 1e7 extents aimed at vertices and edges, and origins beyond the certified
 range (brute-force boxes) -- and hold the GPU to the CPU oracle: face and t bit-exact, colour L_inf < 1e-4.
 """
@@ -73,6 +74,11 @@ FAR_VIEWS = [
     ("soup", 50, (0, 0, 1), "primary", (640, 360)),
     ("soup", 500, (1, -0.5, 1), "primary", (640, 360)),
     ("cube", 500, (0, 0, 1), "full", (320, 240)),
+    # inside the reference-box certificates' origin range (|o2| <= 16 x the largest object coordinate):
+    # certified faces skip the box predicate for these rays
+    ("bunny", 3, (1, 0.5, 1), "full", (480, 360)),
+    ("bunny", 7, (0, 0, 1), "primary", (640, 480)),
+    ("soup", 6, (0.3, 1, 1), "primary", (640, 360)),
 ]
 
 
