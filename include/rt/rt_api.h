@@ -370,6 +370,17 @@ int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
  * each. info[0..6] = binary nodes, binary depth, quantised nodes, quantised depth, triangles reached
  * (binary), triangles reached (quantised), violations (all three trees). RT_OK iff sound. */
 int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]);
+/* Record layout of the device node allocation for a scene of n_nodes binary nodes, n_tris triangle
+ * records and n_wide fp32 4-wide nodes per octant copy (host only, no device): out[0] = allocation bytes
+ * (0: records exceed 4 GiB), out[1] = byte offset of the wide copies (0: the wide tree is dropped because
+ * a wide record offset would reach 2^31, the leaf-handle bit). */
+int rt_debug_record_layout(int64_t n_nodes, int64_t n_tris, int64_t n_wide, int64_t out[2]);
+/* The accept path's shortcuts (host data, no device needed): counts[0] = triangle records, counts[1] =
+ * those whose interpolated normal is certified non-zero, counts[2] = those with a reference-box
+ * certificate; *cert_origin_max (may be NULL) = the object-space origin range (max norm) within which
+ * certified faces skip the box predicate; face_flags (may be NULL, else n_faces entries) = per face the
+ * OR of its records' flag bits (0x80000000 safe normal, 0x40000000 box certificate). */
+int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float* cert_origin_max, uint32_t* face_flags);
 
 /* Kernel-variant override (tests and A/B measurements only; default 0 = the measured-best kernels):
  * same bits as the RT_KERNEL_VARIANT environment variable (1 VGPR wave stack, 2 4-wide quantised

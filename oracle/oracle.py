@@ -42,6 +42,8 @@ def lib():
         L.orc_mesh_from_arrays.argtypes = [C.c_int32, F32P, vp, C.c_int32, I32P, U32P, I32P, C.c_int32,
                                            F32P, C.POINTER(vp)]
         L.orc_mesh_free.argtypes = [vp]
+        L.orc_mesh_set_model.argtypes = [vp, F32P]
+        L.orc_mesh_set_model.restype = None
         L.orc_mesh_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.orc_mesh_export.argtypes = [vp] + [vp] * 8
         L.orc_generate_soup.argtypes = [C.c_int32, C.c_uint64, F32P]
@@ -103,6 +105,10 @@ class Mesh:
                                           mats.reshape(-1) if len(mats) else np.zeros(12, np.float32),
                                           C.byref(h)))
         return cls(h)
+
+    def set_model(self, model16):
+        """Model::modelMatrix (column-major 4x4 affine): getShapeModelMatrix() = model16 * normalisation."""
+        lib().orc_mesh_set_model(self.h, np.ascontiguousarray(model16, np.float32).reshape(16))
 
     def counts(self):
         a, b, c = C.c_int32(), C.c_int32(), C.c_int32()

@@ -326,30 +326,38 @@ static void compute_normals(orc_mesh* m, int32_t ng, const int32_t* gcount, cons
   }
 }
 
-/* derived per-mesh data: shape-model matrix, hoisted invariants */
-static int mesh_finish(orc_mesh* m) {
-  /* normalizeModelMatrix (model.hpp:169-173), getShapeModelMatrix (model.hpp:102-105) */
-  float shape[16], model[16], negc[3] = {-m->center[0], -m->center[1], -m->center[2]};
+/* the model-matrix-dependent data: getShapeModelMatrix() = modelMatrix * shapeMatrix (model.hpp:102-105)
+ * with shapeMatrix from normalizeModelMatrix (model.hpp:169-173), its inverse, the world vertices and the
+ * plane distances (hoisted from calculateDistance, flyscene.cpp:444-478) */
+static void mesh_place(orc_mesh* m, const float* model) {
+  float shape[16], negc[3] = {-m->center[0], -m->center[1], -m->center[2]};
   e_identity(shape); e_scale(shape, m->scale); e_translate(shape, negc);
-  e_identity(model);
   e_affmul(model, shape, m->M);
   e_affinv(m->M, m->Minv);
   for (int j = 0; j < 3; j++) for (int i = 0; i < 3; i++) m->MS[j * 3 + i] = m->Minv[j * 4 + i];
+  for (int32_t i = 0; i < m->nv; i++) e_affv3(m->M, &m->v[4 * i], &m->wv[3 * i]);
+  for (int32_t f = 0; f < m->nf; f++) m->fdist[f] = e_dot(&m->fnn[3 * f], &m->wv[3 * m->f[3 * f]]);
+}
+
+/* derived per-mesh data: shape-model matrix, hoisted invariants */
+static int mesh_finish(orc_mesh* m) {
+  float model[16];
+  e_identity(model);  /* Model::modelMatrix as loaded: identity */
   m->wv = (float*)malloc(sizeof(float) * 3 * (size_t)(m->nv ? m->nv : 1));
   m->nn = (float*)malloc(sizeof(float) * 3 * (size_t)(m->nv ? m->nv : 1));
   m->fnn = (float*)malloc(sizeof(float) * 3 * (size_t)(m->nf ? m->nf : 1));
   m->fdist = (float*)malloc(sizeof(float) * (size_t)(m->nf ? m->nf : 1));
   if (!m->wv || !m->nn || !m->fnn || !m->fdist) { set_err("out of memory", NULL); return -1; }
-  for (int32_t i = 0; i < m->nv; i++) {
-    e_affv3(m->M, &m->v[4 * i], &m->wv[3 * i]);
-    e_normalized(&m->vn[3 * i], &m->nn[3 * i]);
-  }
-  for (int32_t f = 0; f < m->nf; f++) {
-    e_normalized(&m->fn[3 * f], &m->fnn[3 * f]);
-    m->fdist[f] = e_dot(&m->fnn[3 * f], &m->wv[3 * m->f[3 * f]]);
-  }
+  for (int32_t i = 0; i < m->nv; i++) e_normalized(&m->vn[3 * i], &m->nn[3 * i]);
+  for (int32_t f = 0; f < m->nf; f++) e_normalized(&m->fn[3 * f], &m->fnn[3 * f]);
+  mesh_place(m, model);
   return 0;
 }
+
+/* Model::modelMatrix set by the caller (model.hpp: an Affine3f the application may rotate / scale; the
+ * face normals stay the loaded object-space ones, as in the reference, whose calculateDistance uses
+ * getFace().normal against world vertices). model16: column-major 4x4 affine. Build scenes afterwards. */
+void orc_mesh_set_model(orc_mesh* m, const float* model16) { mesh_place(m, model16); }
 
 /* createFaces (mesh.hpp:448-482) + common tail of loadObjFile (objimporter.hpp:284-336) */
 static int mesh_build(orc_mesh* m, int32_t ng, const int32_t* gcount, const uint32_t* idx,

@@ -37,6 +37,9 @@ int orc_mesh_from_arrays(int32_t nv, const float* v3, const float* vn3_or_null, 
                          const int32_t* group_material, int32_t n_materials, const float* mat12,
                          orc_mesh** out);
 void orc_mesh_free(orc_mesh* m);
+/* Model::modelMatrix (column-major affine 4x4; default identity): the shape-model matrix becomes
+ * model16 * normalisation; world vertices and plane distances follow. Build scenes afterwards. */
+void orc_mesh_set_model(orc_mesh* m, const float* model16);
 void orc_mesh_counts(const orc_mesh* m, int32_t* nv, int32_t* nf, int32_t* nm);
 /* any pointer may be NULL. v4:[nv][4] vn3:[nv][3] fidx:[nf][3] fn3:[nf][3] fmat:[nf] mats:[nm][12]
  * M16: shape-model matrix (column-major 4x4), sc4: normalization scale + object centre */

@@ -14,7 +14,9 @@
 namespace {
 
 constexpr char kMagic[8] = {'R', 'T', 'S', 'C', 'E', 'N', 'E', '1'};
-constexpr uint32_t kVersion = 2;  // 2: + object-space vertices (RT_MODE_BOX_COLORS)
+// 2: + object-space vertices (RT_MODE_BOX_COLORS); 3: the header's builder field (version-2 files held 0
+// there, which would read as RT_BUILDER_SAH whatever built them, so they are refused and rebuilt)
+constexpr uint32_t kVersion = 3;
 
 struct Header {
   char magic[8];
@@ -226,11 +228,19 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
       if (hs.fidx[3 * (size_t)f + k] >= (uint32_t)h.nv) { rt::set_error("rt_scene_load: bad face table"); return RT_ERR_IO; }
     if (hs.fmat[f] < -1 || hs.fmat[f] >= h.n_mats) { rt::set_error("rt_scene_load: bad material id"); return RT_ERR_IO; }
   }
+  for (int32_t f = 0; f < h.nf; f++)
+    if (hs.face_box[f] >= (uint32_t)h.n_boxes) { rt::set_error("rt_scene_load: bad face box"); return RT_ERR_IO; }
   for (const rt::TriRec64& t : hs.tris)
-    if (t.face >= (uint32_t)h.nf || (t.box & rt::kBoxIndexMask) >= (uint32_t)h.n_boxes) {
+    if (t.face >= (uint32_t)h.nf || (t.box & rt::kBoxIndexMask) != hs.face_box[t.face]) {
       rt::set_error("rt_scene_load: bad triangle record");
       return RT_ERR_IO;
     }
+  {
+    // the records' flag bits let the kernels skip the normal check and the reference box predicate:
+    // recomputed from the loaded geometry, never taken from the file (a crafted file could set them)
+    const float Ro = rt::cert_origin_max(hs);
+    for (rt::TriRec64& t : hs.tris) t.box = (t.box & rt::kBoxIndexMask) | rt::tri_flags(hs, t.face, Ro);
+  }
   auto handle_ok = [&](uint32_t c, int32_t n_inner) {
     if (rt::is_leaf(c)) return rt::leaf_first(c) + rt::leaf_count(c) <= (uint32_t)h.n_tris;
     return c < (uint32_t)n_inner;

@@ -180,8 +180,16 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 // its extent (what a box prefilter would keep); some lane passed the reference's edge tests. ST_WE1 / ST_WE2:
 // the staged edge tests (RT_TRI_STAGED) left no candidate after the first / the second edge
 enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WPOP, ST_WCULL, ST_WWIDE,
-       ST_WCAND, ST_WPRE, ST_WINS, ST_WE1, ST_WE2, ST_COUNT };
-constexpr int kStatSlots = 16;
+       ST_WCAND, ST_WPRE, ST_WINS, ST_WE1, ST_WE2,
+       // round 4: the same triangle-stage counts with the candidates restricted to the lanes whose ray entered
+       // the leaf's box (ST_WCANDM .. ST_WINSM), the triangle tests of leaves reached by descent (ST_WTRID) and
+       // their entry-masked candidate count (ST_WCANDD: popped leaves unmasked), and wave-level tests where a
+       // lane that never entered the leaf accepted (ST_WACCX: 0 if leaf-entry masking is exact)
+       ST_WCANDM, ST_WE1M, ST_WE2M, ST_WINSM, ST_WTRID, ST_WCANDD, ST_WACCX,
+       // RT_STATS_FRUSTUM experiment: child tests where some lane's own slab test enters but the packet's
+       // interval test does not (must stay 0: the interval test is conservative)
+       ST_WFVIOL, ST_COUNT };
+constexpr int kStatSlots = 24;
 
 struct Hit {
   float t;
@@ -382,7 +390,8 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
 #endif
 template <bool ANY, bool STATS = false>
 __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, uint32_t slot, const Ray& r,
-                                         uint64_t act, Hit& h, bool& found, uint32_t* cnt = nullptr) {
+                                         uint64_t act, Hit& h, bool& found, uint32_t* cnt = nullptr,
+                                         uint64_t entry = ~0ull, bool desc = false) {
   const f3 n{tr.nx, tr.ny, tr.nz};
   const float dn = dot(n, r.d);                 // facenormal.dot(dir)
   const float orth = tr.dist - dot(r.o, n);     // distancePlane - origin.dot(facenormal)
@@ -402,9 +411,22 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
               (fmask<kFcmpOLT>(t, h.t) | (fmask<kFcmpOEQ>(t, h.t) & __builtin_amdgcn_uicmp(tr.rank, h.rank, kIcmpULT)));
   }
   if (STATS) cnt[ST_WCAND] += cand != 0;
-  if (cand == 0) return;
   const f3 p{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
   const f3 w0{tr.w0x, tr.w0y, tr.w0z}, w1{tr.w1x, tr.w1y, tr.w1z}, w2{tr.w2x, tr.w2y, tr.w2z};
+  if (STATS) {
+    // entry-masked stage counts: all three edge masks evaluated for every lane, the stages derived
+    const uint64_t cm = cand & entry;
+    const uint64_t b0 = ballot(dot(n, cross(sub(w1, w0), sub(p, w0))) < 0);
+    const uint64_t b1 = ballot(dot(n, cross(sub(w2, w1), sub(p, w1))) < 0);
+    const uint64_t b2 = ballot(dot(n, cross(sub(w0, w2), sub(p, w2))) < 0);
+    cnt[ST_WCANDM] += cm != 0;
+    cnt[ST_WE1M] += cm != 0 && (cm & ~b0) == 0;
+    cnt[ST_WE2M] += (cm & ~b0) != 0 && (cm & ~b0 & ~b1) == 0;
+    cnt[ST_WINSM] += (cm & ~b0 & ~b1 & ~b2) != 0;
+    if (desc) cnt[ST_WTRID]++;
+    cnt[ST_WCANDD] += (cand & (desc ? entry : ~0ull)) != 0;
+  }
+  if (cand == 0) return;
   if (STATS) {
     const f3 lo{fminf(fminf(w0.x, w1.x), w2.x), fminf(fminf(w0.y, w1.y), w2.y), fminf(fminf(w0.z, w1.z), w2.z)};
     const f3 hi{fmaxf(fmaxf(w0.x, w1.x), w2.x), fmaxf(fmaxf(w0.y, w1.y), w2.y), fmaxf(fmaxf(w0.z, w1.z), w2.z)};
@@ -444,6 +466,7 @@ __device__ __forceinline__ void test_tri(const DevScene& P, const TriRec64& tr, 
   if (STATS) cnt[ST_WINS] += cand != 0;
   if (cand == 0) return;
   const bool acc = lane_in(accept_candidate(P, tr, slot, e0, e2, a0, a1, a2, p, r, cand));
+  if (STATS) cnt[ST_WACCX] += (ballot(acc) & ~entry) != 0;
   if (ANY) {
     found = found | acc;
   } else {
@@ -520,15 +543,63 @@ constexpr int order_bit() {
 }
 #define RT_STR2(x) #x
 #define RT_STR(x) RT_STR2(x)
+// RT_STATS_FRUSTUM (counting-run experiment, ablib builds only): the closest-hit octant loops of the
+// counting run descend by a conservative wave-uniform interval test of the packet (common origin, the
+// interval of each reciprocal direction component over the wave, the wave's largest t_best) instead of
+// the union of the per-lane slab tests; triangle tests stay per lane, so the frame is unchanged and the
+// counters say how many node steps / triangle records that test visits.
+#ifndef RT_STATS_FRUSTUM
+#define RT_STATS_FRUSTUM 0
+#endif
+__device__ __forceinline__ float wave_minf(float v) {
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+struct Frustum {
+  f3 o, idmin, idmax;
+};
+// min / max over id in [a, b] of c * id
+__device__ __forceinline__ float imul_min(float c, float a, float b) { return c >= 0.0f ? c * a : c * b; }
+__device__ __forceinline__ float imul_max(float c, float a, float b) { return c >= 0.0f ? c * b : c * a; }
+template <int OCT>
+__device__ __forceinline__ bool frustum_enter(const Frustum& F, float lx, float hx, float ly, float hy, float lz, float hz,
+                                              float T) {
+  const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
+  const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
+  const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
+  const float tn = fmaxf(fmaxf(imul_min(nx - F.o.x, F.idmin.x, F.idmax.x), imul_min(ny - F.o.y, F.idmin.y, F.idmax.y)),
+                         fmaxf(imul_min(nz - F.o.z, F.idmin.z, F.idmax.z), 0.0f));
+  const float tf = fminf(fminf(imul_max(fx - F.o.x, F.idmin.x, F.idmax.x), imul_max(fy - F.o.y, F.idmin.y, F.idmax.y)),
+                         fminf(imul_max(fz - F.o.z, F.idmin.z, F.idmax.z), T));
+  return tn <= tf;
+}
+
 template <bool ANY, bool STATS, bool STACK_LDS, int OCT = -1>
 __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                          uint32_t* lds_stack, uint32_t* cnt) {
   if (P.n_nodes == 0) return;
+  constexpr bool FRU = RT_STATS_FRUSTUM && STATS && !ANY && OCT >= 0;
+  Frustum F{};
+  bool fru = false;  // the packet has one common origin (primary rays): the interval test drives descent
+  if (FRU) {
+    const float ox = __shfl(r.o.x, (int)__builtin_ctzll(ballot(active) | (1ull << 63)), 64);
+    const float oy = __shfl(r.o.y, (int)__builtin_ctzll(ballot(active) | (1ull << 63)), 64);
+    const float oz = __shfl(r.o.z, (int)__builtin_ctzll(ballot(active) | (1ull << 63)), 64);
+    fru = ballot(active && (r.o.x != ox || r.o.y != oy || r.o.z != oz)) == 0 && ballot(active) != 0;
+    F.o = f3{ox, oy, oz};
+    F.idmin = f3{wave_minf(active ? r.id.x : INFINITY), wave_minf(active ? r.id.y : INFINITY), wave_minf(active ? r.id.z : INFINITY)};
+    F.idmax = f3{wave_maxf(active ? r.id.x : -INFINITY), wave_maxf(active ? r.id.y : -INFINITY), wave_maxf(active ? r.id.z : -INFINITY)};
+  }
   uint32_t stackv = 0;     // lane k holds stack entry k (VGPR stack)
   int sp = 0;              // wave-uniform stack depth (SGPR)
   uint64_t flagstack = 0;  // STATS: per-lane "my ray wanted this entry" bit per stack level
   float tstack[STATS ? 64 : 1];  // STATS: per-lane entry distance into each stack entry
   bool want = active;      // STATS: this lane's ray intersects the current node
+  bool desc = false;       // STATS: the current node was reached by descent (not popped)
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
   uint64_t act = ballot(active);  // lanes still tracing (wave-uniform mask)
@@ -557,7 +628,16 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
         asm volatile("" ::"s"(mm));
       }
 #endif
-      const uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
+      uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
+      const uint64_t lm0 = m0, lm1 = m1;  // the lanes' own verdicts (want flags)
+      if (FRU && fru) {
+        const float T = wave_maxf(active ? h.t : -INFINITY);
+        const bool f0 = frustum_enter<OCT>(F, nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, T);
+        const bool f1 = frustum_enter<OCT>(F, nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, T);
+        cnt[ST_WFVIOL] += (m0 != 0 && !f0) + (m1 != 0 && !f1);
+        m0 = f0 ? ~0ull : 0ull;
+        m1 = f1 ? ~0ull : 0ull;
+      }
 #if RT_EXPERIMENT_SALU > 0  // timing experiment only: N extra independent SALU per node step
       exp_s = uniform(exp_s);
       asm volatile(".rept " RT_STR(RT_EXPERIMENT_SALU) "\n\ts_add_u32 %0, %0, 1\n\t.endr" : "+s"(exp_s));
@@ -584,10 +664,11 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
                         : "s"(uniform(far)), "s"(uniform((uint32_t)sp))
                         : "m0");
       if (STATS) {
-        const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
+        const bool h0 = (lm0 >> lane_id()) & 1, h1 = (lm1 >> lane_id()) & 1;
         const bool wf = first0 ? h1 : h0;
         flagstack = (flagstack & ~(1ull << sp)) | ((uint64_t)wf << sp);
         want = first0 ? h0 : h1;
+        desc = true;
         tstack[sp] = first0 ? s1.tmin : s0.tmin;
       }
       sp += ((m0 != 0) & (m1 != 0)) ? 1 : 0;
@@ -602,7 +683,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       }
       for (uint32_t k = 0; k < count; k++) {
         const TriRec64 tr = sload_tri(P.tris, first + k);
-        test_tri<ANY, STATS>(P, tr, first + k, r, act, h, found, cnt);
+        test_tri<ANY, STATS>(P, tr, first + k, r, act, h, found, cnt, STATS ? ballot(want) : ~0ull, desc);
       }
 #ifdef RT_EXPERIMENT_TRIS_TWICE  // timing experiment only: the same leaf tested again (no effect)
       for (uint32_t k = 0; k < count; k++) {
@@ -622,6 +703,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       node = STACK_LDS ? uniform(lds_stack[sp]) : (uint32_t)__builtin_amdgcn_readlane(stackv, sp);
       if (STATS) {
         want = (flagstack >> sp) & 1;
+        desc = false;
         cnt[ST_WPOP]++;
         if (!ANY && ballot(want && tstack[sp] <= h.t) == 0) cnt[ST_WCULL]++;
       }
@@ -2088,7 +2170,7 @@ __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t
   for (int c = 0; c < ST_COUNT; c++) {
     unsigned long long v = cnt[c];
     if (c == ST_WNODE || c == ST_WTRI || c == ST_WPOP || c == ST_WCULL || c == ST_WWIDE || c == ST_WCAND || c == ST_WPRE ||
-        c == ST_WINS || c == ST_WE1 || c == ST_WE2)
+        c == ST_WINS || c == ST_WE1 || c == ST_WE2 || c >= ST_WCANDM)
       v = (lane == 0) ? v : 0;  // wave counts once
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(P.stats + c, v);
@@ -3197,22 +3279,19 @@ int device_upload(rt_scene* s) {
     // base plus a 32-bit byte offset reaches either: with RT_PREFETCH each uploaded node's pad0 / pad1
     // hold the offsets of its children's records (a leaf child: its first triangle)
     const size_t nn = hs.nodes.size(), nt = hs.tris.size();
-    size_t bytes = (nn + nt) * 64;
-    if (bytes > 0xFFFFFFFFull) {  // cannot happen below kMaxFaces (rt_scene_create checks it)
+    // the fp32 4-wide tree's eight octant copies follow, 128-B aligned (one L2 line per record), when
+    // every wide record offset stays below kLeafBit; else the binary tree serves alone (record_layout)
+    const size_t nw = hs.wide.size();
+    uint64_t wide_base = 0;
+    const size_t bytes = (size_t)record_layout(nn, nt, nw, &wide_base);
+    if (bytes == 0 && nn + nt > 0) {  // cannot happen below kMaxFaces (rt_scene_create checks it)
       set_error("scene records exceed 4 GiB (%zu nodes, %zu triangles)", nn, nt);
       return RT_ERR_INVALID;
     }
-    // the fp32 4-wide tree's eight octant copies follow, 128-B aligned (one L2 line per record), when
-    // the whole allocation stays addressable by 32-bit byte offsets; else the binary tree serves alone
-    const size_t nw = hs.wide.size(), wide_base = (bytes + 127) & ~(size_t)127;
+    static_assert(sizeof(Node128) == 128, "wide record size (record_layout)");
     const size_t wide_bytes = 8 * nw * sizeof(Node128);
-    s->wide_base = 0;
-    s->wide_copy_bytes = 0;
-    if (nw > 0 && wide_base + wide_bytes <= 0xFFFFFFFFull) {
-      s->wide_base = (uint32_t)wide_base;
-      s->wide_copy_bytes = (uint32_t)(nw * sizeof(Node128));
-      bytes = wide_base + wide_bytes;
-    }
+    s->wide_base = (uint32_t)wide_base;
+    s->wide_copy_bytes = wide_base ? (uint32_t)(nw * sizeof(Node128)) : 0;
     if ((rc = dalloc_copy(&s->d_nodes, nullptr, bytes, tot))) return rc;
     std::vector<Node64> nodes(hs.nodes);
     if (RT_PREFETCH) {

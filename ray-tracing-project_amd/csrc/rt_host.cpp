@@ -1280,14 +1280,64 @@ void world_bounds(const HostScene& hs, float lo[3], float hi[3]) {
 // sin(theta_min / 2), here <= 0.01 diam -- only triangles whose smallest angle has sin(theta/2) >= 0.01
 // are certified) and the rounding of M / Minv (a similarity) and of X. Uncertified faces and rays
 // beyond Ro take the fast path and, where it fails, the exact test, as before.
+bool model_is_similarity(const float* M);
 float cert_origin_max(const HostScene& hs) {
+  if (!model_is_similarity(hs.M)) return 0.0f;  // no certificates (box_certified needs Ro > 0)
   float R = 0.0f;
   for (float v : hs.ov3) R = std::max(R, std::fabs(v));  // NaN coordinates are skipped by max
   return std::isfinite(R) ? 16.0f * R : 0.0f;
 }
 
+// The argument above holds for the triangle the edge tests actually accept on, which is the world
+// triangle only when the face normal they use (hs.fnn, the caller's face_normals, never transformed by M)
+// is the world triangle's own normal: with a tilted normal n the accepted region is the triangle projected
+// along n onto n's plane, whose vertices move by up to diam * sin(angle(n, geometric normal)). And Minv
+// must be a similarity for object-space distances to be world distances over one scale. So a
+// model matrix whose linear part is not a uniform scale times a rotation certifies nothing
+// (model_is_similarity), and a face certifies only if its normal is within kCertNormalSin of the world
+// triangle's normal, with that projection offset (2 diam sin) added to the margin.
+constexpr double kCertNormalSin = 1e-3;
+bool model_is_similarity(const float* M) {
+  double c[3][3], n2[3];
+  for (int j = 0; j < 3; j++) {
+    for (int k = 0; k < 3; k++) c[j][k] = M[4 * j + k];  // column j of the column-major linear part
+    n2[j] = c[j][0] * c[j][0] + c[j][1] * c[j][1] + c[j][2] * c[j][2];
+    if (!std::isfinite(n2[j]) || !(n2[j] > 0.0)) return false;
+  }
+  for (int j = 0; j < 3; j++) {
+    if (std::fabs(n2[j] - n2[0]) > 1e-5 * n2[0]) return false;
+    const int i = (j + 1) % 3;
+    const double d = c[j][0] * c[i][0] + c[j][1] * c[i][1] + c[j][2] * c[i][2];
+    if (std::fabs(d) > 1e-5 * n2[0]) return false;
+  }
+  return M[3] == 0.0f && M[7] == 0.0f && M[11] == 0.0f && M[15] == 1.0f;
+}
+
+// sin of the angle between the face normal the edge tests use and the world triangle's normal (2 on
+// degenerate or non-finite input: never certified)
+static double face_normal_tilt(const HostScene& hs, uint32_t f) {
+  double w[3][3];
+  for (int j = 0; j < 3; j++) {
+    const f3& p = hs.wv[hs.fidx[3 * f + j]];
+    w[j][0] = p.x; w[j][1] = p.y; w[j][2] = p.z;
+  }
+  const double a[3] = {w[1][0] - w[0][0], w[1][1] - w[0][1], w[1][2] - w[0][2]};
+  const double c[3] = {w[2][0] - w[0][0], w[2][1] - w[0][1], w[2][2] - w[0][2]};
+  const double g[3] = {a[1] * c[2] - a[2] * c[1], a[2] * c[0] - a[0] * c[2], a[0] * c[1] - a[1] * c[0]};
+  const f3& nf = hs.fnn[f];
+  const double n[3] = {nf.x, nf.y, nf.z};
+  const double gg = g[0] * g[0] + g[1] * g[1] + g[2] * g[2], nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+  if (!std::isfinite(gg) || !std::isfinite(nn) || !(gg > 0.0) || !(nn > 0.0)) return 2.0;
+  const double x[3] = {g[1] * n[2] - g[2] * n[1], g[2] * n[0] - g[0] * n[2], g[0] * n[1] - g[1] * n[0]};
+  const double dn = g[0] * n[0] + g[1] * n[1] + g[2] * n[2];
+  if (!(dn > 0.0)) return 2.0;  // opposite orientation: the edge tests' inside is the other side
+  return std::sqrt((x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) / (gg * nn));
+}
+
 static bool box_certified(const HostScene& hs, uint32_t f, float Ro) {
   if (!(Ro > 0.0f) || hs.ov3.empty()) return false;
+  const double tilt = face_normal_tilt(hs, f);
+  if (!(tilt <= kCertNormalSin)) return false;
   const RefBox& b = hs.boxes[hs.face_box[f]];
   double v[3][3];
   for (int j = 0; j < 3; j++)
@@ -1315,11 +1365,17 @@ static bool box_certified(const HostScene& hs, uint32_t f, float Ro) {
     const double lo = b.low[k], hi = b.high[k];
     if (!std::isfinite(lo) || !std::isfinite(hi)) return false;
     const double S = (hi - lo) + std::fabs(lo) + std::fabs(hi);
-    const double need = 1e-5 * (S + Ro) + 1e-30 + 1e-5 * S + 4e-4 * diam;
+    const double need = 1e-5 * (S + Ro) + 1e-30 + 1e-5 * S + 4e-4 * diam + 2.0 * tilt * diam;
     for (int j = 0; j < 3; j++)
       if (!(v[j][k] - lo >= need && hi - v[j][k] >= need)) return false;
   }
   return true;
+}
+
+// the flag bits of face f's triangle records (kSafeNormalBit, kBoxCertBit): derived from the geometry
+// alone, so the scene cache loader recomputes them instead of trusting the file
+uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro) {
+  return (safe_normal(hs, f) ? kSafeNormalBit : 0u) | (box_certified(hs, f, Ro) ? kBoxCertBit : 0u);
 }
 
 // exact-test record of face f (the kernels' TriRec64)
@@ -1334,7 +1390,7 @@ static void tri_record(const HostScene& hs, uint32_t f, TriRec64& r, float Ro) {
   r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
   r.rank = hs.face_rank[f];
   r.face = f;
-  r.box = hs.face_box[f] | (safe_normal(hs, f) ? kSafeNormalBit : 0u) | (box_certified(hs, f, Ro) ? kBoxCertBit : 0u);
+  r.box = hs.face_box[f] | tri_flags(hs, f, Ro);
 }
 
 void face_records(const HostScene& hs, std::vector<TriRec64>& out) {
@@ -1940,7 +1996,12 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->bvh_gpu_ms = s->bvh_gpu_ms;
   o->box_builder = s->box_builder_used;
   o->boxes_gpu_ms = s->boxes_gpu_ms;
-  o->wide_nodes = (int32_t)s->hs.wide.size();
+  {
+    // the wide tree is uploaded only where its record offsets fit below kLeafBit (record_layout)
+    uint64_t wb = 0;
+    rt::record_layout(s->hs.nodes.size(), s->hs.tris.size(), s->hs.wide.size(), &wb);
+    o->wide_nodes = wb ? (int32_t)s->hs.wide.size() : 0;
+  }
   o->wide_depth = s->hs.depth_wide;
   return RT_OK;
 }
@@ -2143,6 +2204,28 @@ struct Validator {
   }
 };
 }  // namespace
+
+extern "C" int rt_debug_record_layout(int64_t n_nodes, int64_t n_tris, int64_t n_wide, int64_t out[2]) {
+  if (!out || n_nodes < 0 || n_tris < 0 || n_wide < 0) { rt::set_error("rt_debug_record_layout: bad argument"); return RT_ERR_INVALID; }
+  uint64_t wb = 0;
+  out[0] = (int64_t)rt::record_layout((uint64_t)n_nodes, (uint64_t)n_tris, (uint64_t)n_wide, &wb);
+  out[1] = (int64_t)wb;
+  return RT_OK;
+}
+
+extern "C" int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float* cert_origin_max, uint32_t* face_flags) {
+  if (!s || !counts) { rt::set_error("rt_debug_scene_flags: null argument"); return RT_ERR_INVALID; }
+  counts[0] = (int64_t)s->hs.tris.size();
+  counts[1] = counts[2] = 0;
+  if (face_flags) memset(face_flags, 0, sizeof(uint32_t) * (size_t)s->hs.nf);
+  for (const rt::TriRec64& t : s->hs.tris) {
+    counts[1] += (t.box & rt::kSafeNormalBit) != 0;
+    counts[2] += (t.box & rt::kBoxCertBit) != 0;
+    if (face_flags && t.face < (uint32_t)s->hs.nf) face_flags[t.face] |= t.box & (rt::kSafeNormalBit | rt::kBoxCertBit);
+  }
+  if (cert_origin_max) *cert_origin_max = rt::cert_origin_max(s->hs);
+  return RT_OK;
+}
 
 extern "C" int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]) {
   if (!s || !info) { rt::set_error("rt_debug_validate_bvh: null argument"); return RT_ERR_INVALID; }

@@ -41,6 +41,23 @@ constexpr uint32_t kSafeNormalBit = 0x80000000u;
 constexpr uint32_t kBoxCertBit = 0x40000000u;
 constexpr uint32_t kBoxIndexMask = 0x3FFFFFFFu;  // TriRec64::box without its flag bits
 
+// Record layout of the one node allocation: binary nodes, then triangle records (together < 4 GiB, so
+// one 32-bit byte offset reaches any record; binary interior handles = node index * 64 < 2^31 since there
+// are fewer interior nodes than references), then -- 128-B aligned -- the fp32 4-wide tree's eight octant
+// copies. A wide interior handle is the byte offset of its record, and bit 31 marks a leaf handle
+// (kLeafBit), so the wide copies are placed only if every wide record offset stays below 2^31 (ADVICE r3:
+// a record at or above 2 GiB would read as a leaf); otherwise the binary tree serves alone.
+// Returns the allocation's bytes (0: the records exceed 4 GiB); *wide_base = 0 when the wide tree is dropped.
+inline uint64_t record_layout(uint64_t n_nodes, uint64_t n_tris, uint64_t n_wide, uint64_t* wide_base) {
+  const uint64_t bytes = (n_nodes + n_tris) * 64;
+  *wide_base = 0;
+  if (bytes > 0xFFFFFFFFull) return 0;
+  const uint64_t wb = (bytes + 127) & ~(uint64_t)127, wide_bytes = 8 * n_wide * 128;
+  if (n_wide == 0 || wb + wide_bytes > (uint64_t)kLeafBit) return bytes;
+  *wide_base = wb;
+  return wb + wide_bytes;
+}
+
 RT_HD bool is_leaf(uint32_t h) { return (h & kLeafBit) != 0; }
 RT_HD uint32_t leaf_first(uint32_t h) { return h & kLeafFirstMask; }
 RT_HD uint32_t leaf_count(uint32_t h) { return ((h >> kLeafCountShift) & 15u) + 1u; }

@@ -73,6 +73,7 @@ void build_wide(HostScene& hs);
 float bvh_pad(const float lo[3], const float hi[3]);
 float scene_static_pad(const HostScene& hs);
 float cert_origin_max(const HostScene& hs);
+uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro);  // kSafeNormalBit | kBoxCertBit of face f
 void set_error(const char* fmt, ...);
 
 }  // namespace rt

@@ -32,6 +32,7 @@ EXPORTS = [
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
     "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
+    "rt_debug_record_layout", "rt_debug_scene_flags",
 ]
 
 
@@ -137,6 +138,8 @@ def lib():
         L.rt_debug_math_host.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_math_device.argtypes = [C.c_int32, C.c_int32, vp, vp]
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
+        L.rt_debug_record_layout.argtypes = [C.c_int64, C.c_int64, C.c_int64, vp]
+        L.rt_debug_scene_flags.argtypes = [vp, vp, vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
         L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_debug_counters.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
@@ -299,10 +302,14 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, backgr
 
 class Scene:
     def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=2,
-                 box_builder=0, wide_tree=0):
+                 box_builder=0, wide_tree=0, shape_model_matrix=None):
+        """shape_model_matrix: the desc's getShapeModelMatrix() override (column-major 4x4), e.g. the oracle's
+        after Mesh.set_model; default the loader's normalisation."""
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
         self.h = C.c_void_p()
         d = mesh.desc()
+        if shape_model_matrix is not None:
+            d.shape_model_matrix[:] = [float(x) for x in np.asarray(shape_model_matrix, np.float32).reshape(16)]
         o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder, box_builder, wide_tree)
         check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
 
@@ -319,6 +326,20 @@ class Scene:
         t = np.zeros((H, W), np.float32) if want_hits else None
         check(lib().rt_frame_download(self.h, W * H, _p(rgb), _p(face), _p(t)))
         return (rgb, face, t) if want_hits else rgb
+
+    def record_flags(self):
+        """rt_debug_scene_flags: (triangle records, with the safe-normal bit, with the box certificate)."""
+        out = np.zeros(3, np.int64)
+        check(lib().rt_debug_scene_flags(self.h, _p(out), None, None))
+        return tuple(int(x) for x in out)
+
+    def face_flags(self):
+        """(per-face OR of the records' flag bits [n_faces] uint32, certificates' object-space origin range)."""
+        out = np.zeros(3, np.int64)
+        ro = C.c_float(0.0)
+        ff = np.zeros(self.info()["n_faces"], np.uint32)
+        check(lib().rt_debug_scene_flags(self.h, _p(out), C.byref(ro), _p(ff)))
+        return ff, float(ro.value)
 
     def counters(self, n=16):
         """Raw counters of the last RT_FRAME_STATS frame (rt_debug_counters): int64 [n]."""
@@ -475,6 +496,13 @@ class Scene:
         if getattr(self, "h", None) and _lib is not None:
             _lib.rt_scene_destroy(self.h)
             self.h = None
+
+
+def record_layout(n_nodes, n_tris, n_wide):
+    """rt_debug_record_layout: (allocation bytes or 0, wide copies' byte offset or 0 = wide tree dropped)."""
+    out = np.zeros(2, np.int64)
+    check(lib().rt_debug_record_layout(n_nodes, n_tris, n_wide, _p(out)))
+    return int(out[0]), int(out[1])
 
 
 def flycam(W, H, dx=0.0, dy=0.0, dz=0.0):

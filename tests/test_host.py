@@ -192,6 +192,30 @@ def test_bvh_trees_sound(rt, case):
     assert r["nodes4"] >= 1 and r["depth4"] <= r["depth2"] and 3 * r["depth4"] + 4 <= 128
 
 
+def test_record_layout_keeps_wide_offsets_below_leaf_bit(rt):
+    # a wide interior handle is its record's byte offset and bit 31 marks a leaf, so
+    # the wide copies are placed only while every record offset stays below 2^31 (else binary tree only)
+    assert rt.record_layout(0, 0, 0) == (0, 0)
+    nb, wb = rt.record_layout(1_145_405, 1_190_000, 400_000)  # the 1M soup's sizes: wide tree placed
+    base = (1_145_405 + 1_190_000) * 64
+    assert wb == (base + 127) // 128 * 128 and nb == wb + 8 * 400_000 * 128
+    for n_wide in (1, 10, 1000):
+        # largest binary + triangle records for which the wide copies still end at or below 2^31
+        room = 2 ** 31 - 8 * n_wide * 128
+        nn = room // 64 // 2
+        nt = room // 64 - nn
+        nb, wb = rt.record_layout(nn, nt, n_wide)
+        assert wb != 0 and wb + 8 * n_wide * 128 - 128 < 2 ** 31 and nb <= 2 ** 31
+        # one more record pushes the last wide record to 2^31: dropped, the binary tree serves alone
+        nb, wb = rt.record_layout(nn, nt + 2, n_wide)
+        assert wb == 0 and nb == (nn + nt + 2) * 64
+    # a ~7M-face SBVH scene (the advisor's case: ~2.2 GiB of binary + triangle records) keeps no wide tree
+    nb, wb = rt.record_layout(8_000_000, 8_300_000, 2_700_000)
+    assert wb == 0 and nb == 16_300_000 * 64
+    # records beyond 4 GiB cannot be addressed at all
+    assert rt.record_layout(2 ** 26, 1, 0) == (0, 0)
+
+
 def test_ppm_writer_format(rt, tmp_path):
     rgb = np.array([[[0.0, 0.5, 1.0], [1.5, -0.25, 0.999]]], np.float32)
     p = tmp_path / "x.ppm"
@@ -351,6 +375,57 @@ def test_scene_cache_rejects_crafted_trees(rt, tmp_path):
     bad.write_bytes(_cache_sign(s4))
     with pytest.raises(rt.RTError, match="bad BVH root"):
         rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
+    # 5. ADVICE r3: the records' flag bits (safe normal, box certificate) are recomputed on load, never
+    # trusted: a file with every flag set loads with the flags the geometry earns
+    want = sc.record_flags()
+    s5 = [bytearray(x) for x in sec]
+    tris = np.frombuffer(bytes(s5[NODES + 2]), "<u4").reshape(-1, 16).copy()
+    tris[:, 15] |= 0xC0000000
+    s5[NODES + 2] = bytearray(tris.tobytes())
+    bad.write_bytes(_cache_sign(s5))
+    assert rt.Scene.load(bad, device=rt.RT_DEVICE_NONE).record_flags() == want
+    # 6. a record whose box index is not its face's reference box is rejected
+    s6 = [bytearray(x) for x in sec]
+    tris = np.frombuffer(bytes(s6[NODES + 2]), "<u4").reshape(-1, 16).copy()
+    nb = struct.unpack_from("<i", s6[0], 28)[0]
+    tris[0, 15] = (tris[0, 15] & 0xC0000000) | ((int(tris[0, 15] & 0x3FFFFFFF) + 1) % max(nb, 2))
+    s6[NODES + 2] = bytearray(tris.tobytes())
+    bad.write_bytes(_cache_sign(s6))
+    with pytest.raises(rt.RTError, match="bad triangle record"):
+        rt.Scene.load(bad, device=rt.RT_DEVICE_NONE)
+
+
+def _rotation(ax_deg, ay_deg):
+    """column-major 4x4 rotation about x then y (an Affine3f modelMatrix)"""
+    a, b = np.radians(ax_deg), np.radians(ay_deg)
+    rx = np.array([[1, 0, 0], [0, np.cos(a), -np.sin(a)], [0, np.sin(a), np.cos(a)]])
+    ry = np.array([[np.cos(b), 0, np.sin(b)], [0, 1, 0], [-np.sin(b), 0, np.cos(b)]])
+    m = np.eye(4)
+    m[:3, :3] = ry @ rx
+    return m.T.astype(np.float32).reshape(16)  # column-major
+
+
+def test_box_certificates_need_a_similarity_and_matching_normals(rt, orc):
+    """the box certificates argue from the world triangle, whose normal is the face normal only
+    under the loader's own normalisation; a rotated or non-uniformly scaled model matrix (the face normals
+    stay the object-space ones, as in the reference) leaves the edge tests' accepted region tilted, so no
+    face may be certified then. A uniform scale keeps them."""
+    path = scene_path("bunny.obj")
+    base = rt.Scene(rt.Mesh.load_obj(path), device=rt.RT_DEVICE_NONE)
+    n, safe, cert = base.record_flags()
+    assert cert > 0.8 * n, (n, safe, cert)
+    cases = {"rotated": _rotation(20, 30), "stretched": np.diag([1.0, 1.0, 1.5, 1.0]).astype(np.float32).reshape(16),
+             "uniform": np.diag([2.0, 2.0, 2.0, 1.0]).astype(np.float32).reshape(16)}
+    for name, model in cases.items():
+        om = orc.Mesh.load_obj(path)
+        om.set_model(model)
+        M16 = om.export()["M16"]
+        sc = rt.Scene(rt.Mesh.load_obj(path), device=rt.RT_DEVICE_NONE, shape_model_matrix=M16)
+        n2, _, cert2 = sc.record_flags()  # references (a spatial-split tree's count depends on the pose)
+        if name == "uniform":
+            assert cert2 > 0.8 * n2, (name, cert2)
+        else:
+            assert cert2 == 0, (name, cert2)
 
 
 def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):

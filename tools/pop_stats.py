@@ -13,7 +13,9 @@ import conftest  # noqa: E402
 rt = conftest.rtamd
 NAMES = ["node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "primary_rays", "hits",
          "total_rays", "wave_pops", "wave_pops_cullable", "wave_wide_fetches", "wave_tri_cand", "wave_tri_prebox",
-         "wave_tri_inside", "wave_tri_exit_edge1", "wave_tri_exit_edge2"]
+         "wave_tri_inside", "wave_tri_exit_edge1", "wave_tri_exit_edge2",
+         "wave_tri_cand_m", "wave_tri_exit_edge1_m", "wave_tri_exit_edge2_m", "wave_tri_inside_m",
+         "wave_tri_desc", "wave_tri_cand_desc_m", "wave_tri_accept_outside_entry", "wave_frustum_violations"]
 
 
 def main(scenes):
@@ -24,12 +26,17 @@ def main(scenes):
         else:
             mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         sc = rt.Scene(mesh, device=0)
-        sc.render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS)
-        out = sc.counters()
+        cam = rt.flycam(W, H, 0, 0, 20)
+        _, face_s, t_s, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS, want_hits=True)
+        out = sc.counters(24)
+        _, face_n, t_n, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, want_hits=True)
         d = {k: out[i] for i, k in enumerate(NAMES)}
         waves = (W // 8) * ((H + 7) // 8)
         d["scene"] = name
         d["waves"] = waves
+        # the counting run's frame against the production kernel's (any traversal experiment must not change it)
+        d["counting_frame_face_mismatches"] = int((face_s != face_n).sum())
+        d["counting_frame_t_mismatches"] = int((t_s.view("u4") != t_n.view("u4")).sum())
         d["pops_per_wave"] = d["wave_pops"] / waves
         d["node_steps_per_wave"] = d["wave_node_fetches"] / waves
         d["cullable_share_of_pops"] = d["wave_pops_cullable"] / max(d["wave_pops"], 1)
@@ -40,6 +47,14 @@ def main(scenes):
         d["tri_share_inside"] = d["wave_tri_inside"] / wt  # some lane past the edge tests
         d["tri_share_exit_edge1"] = d["wave_tri_exit_edge1"] / wt  # staged edge tests: none left after edge 1
         d["tri_share_exit_edge2"] = d["wave_tri_exit_edge2"] / wt
+        # round 4: candidates restricted to the lanes whose ray entered the leaf's box (all leaves / leaves
+        # reached by descent only), and whether any lane outside the entry mask ever accepted (must be 0)
+        d["tri_share_cand_masked"] = d["wave_tri_cand_m"] / wt
+        d["tri_share_exit_edge1_masked"] = d["wave_tri_exit_edge1_m"] / wt
+        d["tri_share_exit_edge2_masked"] = d["wave_tri_exit_edge2_m"] / wt
+        d["tri_share_inside_masked"] = d["wave_tri_inside_m"] / wt
+        d["tri_share_in_descent_leaves"] = d["wave_tri_desc"] / wt
+        d["tri_share_cand_descent_masked"] = d["wave_tri_cand_desc_m"] / wt
         print(json.dumps(d), flush=True)
 
 
