@@ -21,7 +21,7 @@ VERSION_H := $(OBJ)/rt_version.h
 $(shell mkdir -p $(OBJ) && echo '#define RT_SOURCE_HASH "$(SRC_HASH)"' > $(VERSION_H).new && \
         (cmp -s $(VERSION_H).new $(VERSION_H) || cp $(VERSION_H).new $(VERSION_H)); rm -f $(VERSION_H).new)
 
-all: $(LIB) oracle cli
+all: $(LIB) variants oracle cli
 
 $(OBJ)/rt_device.o: $(PKG)/csrc/rt_device.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -30,6 +30,10 @@ $(OBJ)/rt_device.o: $(PKG)/csrc/rt_device.hip $(HDRS)
 $(OBJ)/rt_host.o: $(PKG)/csrc/rt_host.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OBJ)/rt_variants.o: $(PKG)/csrc/rt_variants.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJ)/rt_build.o: $(PKG)/csrc/rt_build.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -46,7 +50,16 @@ $(OBJ)/rt_cache.o: $(PKG)/csrc/rt_cache.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o
+PRODUCT_OBJS := $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o
+$(LIB): $(PRODUCT_OBJS)
+	@mkdir -p $(PKG)/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+# the A/B kernel variants (rt_variants.hip) linked beside the product objects: the same library plus the
+# measured alternatives, for tests/test_gpu_parity.py's variant check and A/B timing (RTAMD_LIB)
+VARLIB := $(PKG)/lib/librtamd_variants.so
+variants: $(VARLIB)
+$(VARLIB): $(PRODUCT_OBJS) $(OBJ)/rt_variants.o
 	@mkdir -p $(PKG)/lib
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
@@ -55,7 +68,8 @@ $(LIB): $(OBJ)/rt_device.o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o 
 ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o
 	@mkdir -p $(OBJ) $(PKG)/lib
 	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $(OBJ)/rt_device_$(TAG).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o -lpthread
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $(PKG)/csrc/rt_variants.hip -o $(OBJ)/rt_variants_$(TAG).o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_variants_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o -lpthread
 
 cli: $(PKG)/lib/rt_render_cli
 
@@ -75,4 +89,4 @@ clean:
 	rm -rf $(OBJ) $(PKG)/lib
 	$(MAKE) -C oracle clean
 
-.PHONY: ablib all oracle cli asm clean
+.PHONY: ablib all variants oracle cli asm clean

@@ -282,6 +282,38 @@ def kernel_bound(kernel):
     return lim, f"profiles/{os.path.basename(best[0])}: {best[1]['limiter']}"
 
 
+DIGESTS = os.path.join(ROOT, "tests", "golden", "fullframe_digests.json")
+SAMPLES = os.path.join(ROOT, "tests", "golden", "fullframe_samples.npz")
+
+
+def frame_parity(rt, sc, W, H, mode, case):
+    """Parity of the frame this bench times, outside the timed region: one render of the
+    same camera with hit records, its per-pixel face ids and t bits hashed (SHA-256) against the oracle's
+    committed full-frame digests (tests/golden/fullframe_digests.json, tools/gen_fullframe_digests.py), and
+    its colours against the committed strided oracle sample (every 257th pixel). No oracle run needed."""
+    import hashlib
+    dig = json.load(open(DIGESTS)).get(case)
+    if dig is None or (dig["W"], dig["H"]) != (W, H) or dig["mode"] != ("full" if mode == rt.RT_MODE_FULL else "primary"):
+        return {"case": case, "face_t_digest_equal": None, "why": "no committed digest of this frame"}
+    rgb, face, t, _ = sc.render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    face_ok, t_ok = sha(face) == dig["face_sha256"], sha(t) == dig["t_sha256"]
+    out = {"case": case, "pixels": W * H, "face_t_digest_equal": bool(face_ok and t_ok),
+           "face_digest_equal": bool(face_ok), "t_digest_equal": bool(t_ok),
+           "hits": int((np.asarray(face) >= 0).sum()), "oracle_hits": dig["hits"]}
+    smp = np.load(SAMPLES)
+    if case + "_idx" in smp:
+        idx = smp[case + "_idx"]
+        a = np.asarray(rgb, np.float64).reshape(-1, 3)[idx]
+        b = smp[case + "_rgb"].astype(np.float64)
+        err = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b))
+        out["colour_linf_sampled"] = float(np.nanmax(err)) if err.size else 0.0
+        out["colour_sample_pixels"] = int(len(idx))
+    out["what"] = ("face ids + t bits of every pixel: SHA-256 against the oracle's committed digests; colour L_inf "
+                   "against the committed oracle sample")
+    return out
+
+
 def side_config(rt, scene_name, mode, steps, warmup, device):
     """A single-GPU BASELINE config beside the headline one: C2 = bunny PRIMARY,
     C5 = bunny FULL, 1920x1080: rate with frames in flight and one frame at a time."""
@@ -300,6 +332,7 @@ def side_config(rt, scene_name, mode, steps, warmup, device):
             sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, flags=rt.RT_FRAME_STATS)
             s2 = sc.synchronize()
             out["total_mrays_per_s"] = round(s2["total_rays"] * steps / el / 1e6, 2)
+            out["parity"] = frame_parity(rt, sc, W, H, m, scene_name)
         del sc
     return out
 
@@ -466,6 +499,8 @@ def main():
         rays2 = reduce(float(st2["primary_rays"] * k2), "SUM")
         extra = {"frame": f"{W2}x{H2}", "workload": "C4 frame on 1 GPU" if n == 1 else f"C3 frame split over {n} GPUs",
                  "mrays_per_s": round(rays2 / el2 / 1e6, 2), "ms_per_step": round(el2 / k2 * 1e3, 4), "steps": k2}
+        if n == 1 and a.tris == 1_000_000 and mode == rt.RT_MODE_PRIMARY:
+            extra["parity"] = frame_parity(rt, sc, W2, H2, mode, "C4")
 
     # the other single-GPU BASELINE configs on the same GPU (N = 1 headline run only)
     side = {}
@@ -483,7 +518,7 @@ def main():
         n_node = stats["node_visits"] / rays
         n_tri = stats["tri_tests"] / rays
         hit = stats["hits"] / rays
-        split = mode == rt.RT_MODE_PRIMARY and (int(os.environ.get("RT_KERNEL_VARIANT", "0") or 0) & (32768 | 256 | 2048))
+        split = mode == rt.RT_MODE_PRIMARY and os.environ.get("RTAMD_DEBUG_KNOBS") == "1" and (int(os.environ.get("RT_KERNEL_VARIANT", "0") or 0) & (32768 | 256 | 2048))
         kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
         # the packet algorithm's bytes per launch: node / triangle records once per wave, the hit lanes'
         # triangle + shading records, the pixel
@@ -515,6 +550,11 @@ def main():
                 # its own records): served from SGPRs / L2 / MALL, not HBM -- reported, not priced
                 "survey_demand_bytes_per_ray": round(64 * n_node + 40 * n_tri + 92 * hit + 12, 1),
                 "n_node": round(n_node, 2), "n_tri": round(n_tri, 2), "hit": round(hit, 4)}
+
+    # the headline frame's parity against the committed oracle digests (every pixel; N = 1, C3)
+    headline_parity = None
+    if rank == 0 and n == 1 and not K and a.frame is None and a.scene == "soup" and a.tris == 1_000_000:
+        headline_parity = frame_parity(rt, sc, W, H, mode, "C3" if a.mode == "primary" else "C3-full")
 
     gpu_frame = None
     if rank == 0 and n == 1 and not a.no_cpu:
@@ -585,6 +625,10 @@ def main():
         if extra is not None:
             out["c4_frame" if n == 1 else "c3_frame"] = extra
         out.update(side)
+        if headline_parity is not None:
+            out["parity"] = headline_parity
+            checked = [headline_parity] + [v["parity"] for v in (side.get("c2"), side.get("c5"), extra) if v and "parity" in v]
+            out["parity_all_configs"] = {p["case"]: p["face_t_digest_equal"] for p in checked}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

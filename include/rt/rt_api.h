@@ -382,12 +382,21 @@ int rt_debug_record_layout(int64_t n_nodes, int64_t n_tris, int64_t n_wide, int6
  * OR of its records' flag bits (0x80000000 safe normal, 0x40000000 box certificate). */
 int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float* cert_origin_max, uint32_t* face_flags);
 
-/* Kernel-variant override (tests and A/B measurements only; default 0 = the measured-best kernels):
- * same bits as the RT_KERNEL_VARIANT environment variable (1 VGPR wave stack, 2 4-wide quantised
- * BVH, 4 XCD-contiguous tile order, 16 FULL as a stage pipeline, +32/64/128 per-lane traversal in
- * its reflection / secondary-shadow / primary-shadow stages). Every variant renders the same bits.
- * Returns the previous value. */
+/* Kernel-variant override (tests and A/B measurements only; default 0 = the measured-best kernels).
+ * Bits of the product library: 4 / 512 / 1536 tile orders, 8192 / 16384 FULL megakernel builds, 32768
+ * PRIMARY as trace + shade kernels, 65536 the generic traceRay kernel, 131072 / 262144 / 524288
+ * longest-first dispatch knobs, 2097152 PRIMARY packets on the binary tree. Bits of the variants library
+ * only (make variants -> librtamd_variants.so; the product library's rt_render returns
+ * RT_ERR_UNSUPPORTED for them): 1 VGPR wave stack, 2 4-wide quantised BVH, 16 FULL as a stage pipeline
+ * (+32/64/128 per-lane traversal in its reflection / secondary-shadow / primary-shadow stages), 256 two
+ * rays per lane, 2048 persistent threads (+4096 no stealing), 1048576 two packets per wave. Every
+ * variant renders the same bits. Returns the previous value. */
 int rt_debug_set_variant(int32_t v);
+/* Diagnostics: on = 1 lets the library read its A/B and diagnostic environment knobs (RT_KERNEL_VARIANT,
+ * RT_SPLIT_K, RT_SPLIT_KP, RT_LDS_PAD, RT_SAH_TRAV, RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_TIMING); by default
+ * (and after on = 0) it ignores the process environment, so a drop-in's trees, kernels and dispatch never
+ * depend on it. Turning it on also takes RT_KERNEL_VARIANT as the current kernel variant. */
+int rt_debug_env_knobs(int32_t on);
 
 /* Wave timeline of the last frame rendered with RT_FRAME_TIMELINE (diagnostics): per wave, in dispatch
  * order (workgroup id), 8 words: shader-clock s_memtime at start (lo, hi) and end (lo, hi), the

@@ -351,7 +351,7 @@ int gpu_build_ref_boxes(int device, HostScene& hs, const float* v4, int32_t min_
   // the passes of generateBoundingBoxes (flyscene.cpp:404-417)
   std::vector<DBox> todo, kids;
   std::vector<size_t> todo_idx;
-  const bool timing = getenv("RT_TIMING") != nullptr;
+  const bool timing = debug_env("RT_TIMING") != nullptr;
   auto tp = std::chrono::steady_clock::now();
   int pass = 0;
   bool notDone = true;

@@ -31,6 +31,10 @@ using rt::f3;
 
 namespace rt {
 static thread_local std::string g_err;
+static std::atomic<bool> g_debug_env{false};
+void set_debug_env(bool on) { g_debug_env.store(on); }
+const char* debug_env(const char* name) { return g_debug_env.load(std::memory_order_relaxed) ? getenv(name) : nullptr; }
+
 void set_error(const char* fmt, ...) {
   char buf[1024];
   va_list ap;
@@ -1471,7 +1475,8 @@ static void relayout_pairs(HostScene& hs, const std::vector<Node64>& tmp, uint32
 }
 
 void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) {
-  static const bool pairs = [] { const char* e = getenv("RT_NODE_LAYOUT"); return e && !strcmp(e, "pairs"); }();
+  const char* layout_env = debug_env("RT_NODE_LAYOUT");
+  const bool pairs = layout_env && !strcmp(layout_env, "pairs");
   if (pairs) { relayout_pairs(hs, tmp, root); return; }
   std::vector<uint32_t> remap(tmp.size(), UINT32_MAX), order;
   std::vector<std::pair<uint32_t, int>> st{{root, 1}};
@@ -1505,7 +1510,8 @@ void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) 
 // SBVH build (SbvhBuilder) from the face references; leaves get their triangle slots depth first (the
 // order the DFS re-layout visits them), so the result does not depend on the build's thread timing
 static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, const Aabb& world, float alpha) {
-  static const float budget = [] { const char* e = getenv("RT_SBVH_BUDGET"); return e ? (float)atof(e) : 0.5f; }();
+  const char* budget_env = debug_env("RT_SBVH_BUDGET");
+  const float budget = budget_env ? (float)atof(budget_env) : 0.5f;
   const int64_t cap = std::min<int64_t>((int64_t)hs.nf + (int64_t)(budget * hs.nf) + 1, (int64_t)kMaxFaces);
   std::vector<Node64> tmp((size_t)cap);
   SbvhBuilder B{hs, tmp};
@@ -1513,7 +1519,7 @@ static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, c
   B.leaf_lists.resize((size_t)cap);
   B.refs = hs.nf;
   B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
-  if (const char* e = getenv("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
+  if (const char* e = debug_env("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
   B.pad = bvh_pad(world.lo, world.hi);
   B.alpha = alpha;
   B.root_area = std::max(world.area(), 1e-30f);
@@ -1557,7 +1563,7 @@ static void build_sbvh(HostScene& hs, int leaf_size, std::vector<Prim>& prims, c
   parallel_chunks(order.size(), [&](size_t sb, size_t se, int) {
     for (size_t i = sb; i < se; i++) tri_record(hs, order[i], hs.tris[i], Ro);
   });
-  if (getenv("RT_TIMING")) {
+  if (debug_env("RT_TIMING")) {
     size_t cert = 0;
     for (const TriRec64& t : hs.tris) cert += (t.box & kBoxCertBit) != 0;
     fprintf(stderr, "[rt] sbvh build %.1f ms: %zu references for %d faces, %u nodes, %zu references box-certified\n",
@@ -1598,10 +1604,10 @@ void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
   BvhBuilder B{prims, tmp};
   B.hw = std::max(1u, std::thread::hardware_concurrency());
   B.leaf_size = std::max(1, std::min(leaf_size, kMaxLeaf));
-  if (const char* e = getenv("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
+  if (const char* e = debug_env("RT_SAH_TRAV")) B.kTrav = std::max(0.05f, (float)atof(e));
   B.pad = bvh_pad(world.lo, world.hi);
   Aabb rootb;
-  const bool timing = getenv("RT_TIMING") != nullptr;
+  const bool timing = debug_env("RT_TIMING") != nullptr;
   auto tb0 = std::chrono::steady_clock::now();
   uint32_t root = B.build(0, (uint32_t)hs.nf, 0, rootb);
   if (timing) fprintf(stderr, "[rt] bvh recursive build %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
@@ -1931,7 +1937,7 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   }
   if (!boxes_done) rt::build_ref_boxes(hs, d->vertices, s->opts.min_faces, s->opts.max_boxes);
   s->boxes_ms = ms_since(t1);
-  if (getenv("RT_TIMING"))
+  if (rt::debug_env("RT_TIMING"))
     fprintf(stderr, "[rt] boxes %.1f ms (%s, device %.1f ms), %zu boxes\n", s->boxes_ms,
             s->box_builder_used == RT_BOXES_GPU ? "gpu" : "host", s->boxes_gpu_ms, hs.boxes.size());
   auto t2 = clk::now();
@@ -1949,7 +1955,7 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     const bool spatial = s->opts.builder == RT_BUILDER_SBVH;
     rt::build_bvh(hs, leaf, spatial);
     s->builder_used = spatial ? RT_BUILDER_SBVH : RT_BUILDER_SAH;
-    if (getenv("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));
+    if (rt::debug_env("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));
     rt::build_bvh4(hs);
   }
   if (s->opts.wide_tree) rt::build_wide(hs);  // fp32 4-wide collapse of the binary tree (PRIMARY packets)

@@ -32,7 +32,7 @@ EXPORTS = [
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
     "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
-    "rt_debug_record_layout", "rt_debug_scene_flags",
+    "rt_debug_record_layout", "rt_debug_scene_flags", "rt_debug_env_knobs",
 ]
 
 
@@ -141,6 +141,11 @@ def lib():
         L.rt_debug_record_layout.argtypes = [C.c_int64, C.c_int64, C.c_int64, vp]
         L.rt_debug_scene_flags.argtypes = [vp, vp, vp, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
+        L.rt_debug_env_knobs.argtypes = [C.c_int32]
+        # A/B and diagnostic environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SAH_TRAV, RT_TIMING, ...):
+        # the library ignores the environment unless asked; measurement scripts opt in explicitly
+        if os.environ.get("RTAMD_DEBUG_KNOBS") == "1":
+            L.rt_debug_env_knobs(1)
         L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_debug_counters.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, scene_path
+from conftest import GOLDEN, ROOT, scene_path
 from test_oracle_pinning import read_kat, same_bits
 
 pytestmark = pytest.mark.gpu
@@ -200,32 +200,79 @@ def test_stats_counting_run(rt, soup):
     assert st["wave_node_fetches"] * 16 < st["node_visits"]  # coherence: one fetch serves many rays
 
 
-VARIANTS = {"vgpr-stack": 1, "wide4": 2, "xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-pipeline": 16, "pipeline-lane-refl": 48,
-            "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
-            "persistent-no-steal": 2048 | 4096, "full-8-waves": 8192, "full-small-build": 16384,
-            "split-primary": 32768, "generic-depth-kernel": 65536, "dual-chain": 1048576}
+# variant bits the product library serves itself (rt_api.h rt_debug_set_variant)
+VARIANTS = {"xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-8-waves": 8192, "full-small-build": 16384,
+            "split-primary": 32768, "generic-depth-kernel": 65536}
+# the A/B kernels of the variants library only (rt_variants.hip, `make variants`)
+VARIANTS_LIB = {"vgpr-stack": 1, "wide4": 2, "full-pipeline": 16, "pipeline-lane-refl": 48,
+                "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
+                "persistent-no-steal": 2048 | 4096, "dual-chain": 1048576}
 
 
-@pytest.mark.parametrize("name", sorted(VARIANTS))
-def test_kernel_variants_render_identical_bits(rt, soup, name):
-    """Every A/B kernel variant (traversal flavour, FULL megakernel vs stage pipeline, per-lane walks)
-    renders exactly the default kernels' frame (rgb, face, t) on bunny (PRIMARY + FULL) and the 1M soup
-    (FULL, 640x360 crop of the C3 camera)."""
-    sc_soup, _ = soup
-    bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+def variant_frames_identical(rt, scenes, bits):
+    """Render bunny (PRIMARY + FULL, 1080p) and the 1M soup (FULL 640x360, PRIMARY 1000x563) with the default
+    kernels and with kernel variant `bits`; returns the cases whose rgb / face / t differ."""
+    bunny, soup = scenes
     cases = [(bunny, 1920, 1080, rt.RT_MODE_PRIMARY), (bunny, 1920, 1080, rt.RT_MODE_FULL),
-             (sc_soup, 640, 360, rt.RT_MODE_FULL), (sc_soup, 1000, 563, rt.RT_MODE_PRIMARY)]
+             (soup, 640, 360, rt.RT_MODE_FULL), (soup, 1000, 563, rt.RT_MODE_PRIMARY)]
+    bad = []
     for sc, W, H, m in cases:
         cam = rt.flycam(W, H, 0, 0, 20)
         prev = rt.set_variant(0)
         try:
             ref = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
-            rt.set_variant(VARIANTS[name])
+            rt.set_variant(bits)
             got = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
         finally:
             rt.set_variant(prev)
-        for a, b in zip(ref[:3], got[:3]):
-            assert np.asarray(a).tobytes() == np.asarray(b).tobytes(), (name, W, H, m)
+        if any(np.asarray(a).tobytes() != np.asarray(b).tobytes() for a, b in zip(ref[:3], got[:3])):
+            bad.append((W, H, m))
+    return bad
+
+
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+def test_kernel_variants_render_identical_bits(rt, soup, name):
+    """Every kernel variant of the product library (tile orders, FULL builds, the two-kernel PRIMARY, the
+    generic traceRay kernel) renders exactly the default kernels' frame (rgb, face, t) on bunny (PRIMARY +
+    FULL) and the 1M soup (FULL, 640x360 crop of the C3 camera)."""
+    bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    assert variant_frames_identical(rt, (bunny, soup[0]), VARIANTS[name]) == []
+
+
+def test_product_library_refuses_variant_only_kernels(rt, soup):
+    """The A/B kernels (VGPR stack, quantised 4-wide tree, FULL pipeline, two rays per lane, persistent
+    threads, dual chain) are not in the product library: selecting one fails loudly instead of silently
+    rendering with the default kernels."""
+    sc, _ = soup
+    cam = rt.flycam(64, 64, 0, 0, 20)
+    for name, bits in sorted(VARIANTS_LIB.items()):
+        prev = rt.set_variant(bits)
+        try:
+            mode = rt.RT_MODE_FULL if bits & 16 else rt.RT_MODE_PRIMARY
+            with pytest.raises(rt.RTError, match="A/B build option"):
+                sc.render(cam, rt.DEFAULT_LIGHTS, 64, 64, mode=mode)
+        finally:
+            rt.set_variant(prev)
+
+
+def test_variants_library_renders_identical_bits(rt):
+    """Every A/B kernel of the variants library (rt_variants.hip) renders the default kernels' frames bit for
+    bit: tests/variants_check.py in a child process with RTAMD_LIB = lib/librtamd_variants.so (one library
+    per process), the same four frames per variant as above."""
+    import json
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, "ray-tracing-project_amd", "lib", "librtamd_variants.so")
+    if not os.path.exists(lib):
+        pytest.skip("variants library not built (make variants)")
+    env = dict(os.environ, RTAMD_LIB=lib)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "variants_check.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert set(res) == set(VARIANTS_LIB), res
+    bad = {k: v for k, v in res.items() if v}
+    assert not bad, bad
 
 
 def test_frames_in_flight_are_independent(rt, soup):

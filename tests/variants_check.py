@@ -1,0 +1,32 @@
+"""Child process of test_variants_library_renders_identical_bits (tests/test_gpu_parity.py): loads the
+library named by RTAMD_LIB (lib/librtamd_variants.so: the product kernels plus the A/B kernels of
+rt_variants.hip) and renders, for every A/B variant, bunny (PRIMARY + FULL, 1080p) and the 1M soup (FULL
+640x360, PRIMARY 1000x563) with the default kernels and with the variant. Prints one JSON line:
+{variant name: [differing cases]}. Not a test module (no test_ functions); needs a GPU."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import conftest  # noqa: E402  (loads ray-tracing-project_amd/rtamd.py, honouring RTAMD_LIB)
+from conftest import scene_path  # noqa: E402
+from test_gpu_parity import VARIANTS_LIB, variant_frames_identical  # noqa: E402
+
+
+def main():
+    rt = conftest.rtamd
+    assert os.path.basename(rt.LIB_PATH).startswith("librtamd_variants"), rt.LIB_PATH
+    bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    mesh, _, _ = rt.soup_mesh(1_000_000)
+    soup = rt.Scene(mesh)
+    out = {}
+    for name, bits in sorted(VARIANTS_LIB.items()):
+        out[name] = [list(map(int, c)) for c in variant_frames_identical(rt, (bunny, soup), bits)]
+        print(f"{name}: {'identical' if not out[name] else out[name]}", file=sys.stderr, flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Node layout A/B: depth-first (default) vs sibling pairs in one 128-B line (RT_NODE_LAYOUT=pairs).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

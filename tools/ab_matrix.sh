@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B matrix on the bench workload (GPU box): library builds x RT_KERNEL_VARIANT values, one frame in
 # flight (isolated kernels) with the counting run, so node/triangle counts come with each time.
 #   RUNS="default:0 default:512 order:0" FIF=1 bash tools/ab_matrix.sh

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B of the spatial-split BVH (RT_SBVH=<alpha>) against the binned-SAH tree: GPU parity suite with the
 # SBVH scenes first, then interleaved bench runs (the scene is built inside each bench process).
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B of FrameParams::split_k (RT_SPLIT_K: the costliest waves of lone FULL frames as 16-lane sub-waves):
 # parity tests first, then C5 (bunny FULL) and the soup FULL one frame at a time, and C5 at 4 in flight.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B of kernel variants (RT_KERNEL_VARIANT) x library builds, one frame in flight (isolated kernels)
 # and the default frames in flight: VARIANTS="0 256" LIBS="default x2w8"
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B of kernel variants (RT_KERNEL_VARIANT values) and library builds on bench workloads, interleaved
 # over REPS rounds. VARS="0 1048576"; LIBS="default dual6"; CFGS="soup:primary:1 ..." (scene:mode:fif).
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Round 3 A/B: fp32 4-wide tree prefetch forms (librtamd_wpf*.so) vs the default build and the binary tree
 # (RT_KERNEL_VARIANT=2097152); C3 at 4 frames in flight and one frame at a time; then one SQ counter pass
 # each for the wide default and the binary tree (one frame in flight).

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B of library builds on the FULL configurations (GPU box): LIBS="default fw4 ...", VARIANT env
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # FULL-mode A/B (GPU box): parity tests, then bench of bunny/soup FULL per RT_KERNEL_VARIANT in VARIANTS
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # FULL megakernel occupancy A/B (GPU box): library builds x RT_KERNEL_VARIANT on bunny (C5) and the soup.
 #   RUNS="bunny:default:0 bunny:small7:0 bunny:default:8192 soup:default:0 soup:big6:0" bash tools/full_occ_ab.sh
 set -u

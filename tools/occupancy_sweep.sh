@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Occupancy experiment (diagnostics): the C3 bench with the fused PRIMARY kernel capped at fewer resident
 # waves per CU by padding its LDS (RT_LDS_PAD bytes per one-wave block: 160 KiB / (pad + ~1 KiB) blocks
 # per CU). Answers how much throughput the kernel gains per extra resident traversal chain.

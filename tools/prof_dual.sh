@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Counter comparison of the single-chain fused PRIMARY kernel and the dual-chain variant (C3, one frame
 # in flight): issue / wait split, instruction and scalar-cache counts.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Scalar-memory latency and scalar-cache pressure of the fused PRIMARY kernel (C3, one frame in flight):
 # SQ_INST_LEVEL_SMEM / SQ_INSTS_SMEM = mean SMEM latency in cycles; SQC busy / stall counters.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Round 3: far-origin exactness tests with the per-ray culling pad (default build) and with the static pad
 # only (librtamd_nopad.so, RT_DYN_PAD=0), then the whole GPU suite and the C3 / C5 bench lines.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Round 3: SBVH traversal-cost constant (RT_SAH_TRAV) and leaf bound (--leaf) re-swept after the triangle
 # test got cheaper (staged edge tests, box certificates). One JSON line per run under gpurun_out/<TAG>/.
 set -u

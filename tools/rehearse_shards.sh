@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # Strong-scaling rehearsal on one GPU: the C4 frame's shard 0 of K (K = 1, 2, 4, 8), i.e. the per-GPU work
 # of a K-GPU run without the collective; efficiency = K x shard rate / the whole frame's rate.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # SAH cost ratio on the bunny configurations (GPU box): TRAVS="1 0.7" bash tools/sah_bunny.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # SAH cost-ratio sweep (RT_SAH_TRAV) x leaf cap on the bench workload (GPU box). SAH="trav:leaf ..."
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

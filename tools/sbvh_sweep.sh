@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # SBVH parameter sweep on the C3 soup (bench.py builds the scene in-process): combos of
 # RT_SBVH (alpha) / RT_SBVH_BUDGET / RT_SAH_TRAV given as "alpha:budget:trav" in COMBOS.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export RTAMD_DEBUG_KNOBS=1  # the library reads RT_* knobs only when asked (rt_debug_env_knobs)
 # A/B sweep of kernel variants and BVH leaf sizes on the bench workload (GPU box).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
