@@ -1,9 +1,18 @@
-// rt_build.hip -- GPU LBVH builder: Morton codes of the triangle centroids, a device
-// radix sort (hipCUB), Karras' parallel radix-tree construction (one thread per interior node), bottom-up
-// bounds with agent-scope acquire/release counters, then one Node64 per interior node with subtrees of
-// <= leaf_size triangles collapsed into leaf handles. Child boxes get the same conservative padding as
-// the host builder, so traversal stays exact. Build time is milliseconds instead of the host SAH's
-// ~1 s at 1M triangles; the tree is shallower-quality (no SAH), traded for build speed.
+// rt_build.hip -- GPU BVH builders (SURVEY.md 8(f) f2 "LBVH/PLOC").
+// LBVH: Morton codes of the triangle centroids, a device radix sort (hipCUB), Karras' parallel radix-tree
+// construction (one thread per interior node), bottom-up bounds with agent-scope acquire/release
+// counters, then one Node64 per interior node with subtrees of <= leaf_size triangles collapsed into leaf
+// handles. Build time is milliseconds instead of the host SAH's ~1 s at 1M triangles; the tree is
+// lower-quality (no SAH), traded for build speed.
+// PLOC (Meister & Bittner, "Parallel Locally-Ordered Clustering for Bounding Volume Hierarchy
+// Construction", TVCG 2018): the Morton-sorted triangles are clusters; every iteration each cluster finds
+// its nearest neighbour (smallest surface area of the merged box) among the `radius` clusters either side
+// in Morton order, mutual nearest neighbours merge into a new interior node, and the cluster array is
+// compacted in order -- until one cluster is left. Agglomerative clustering by surface area gives trees of
+// SAH quality at GPU speed. A bottom-up SAH pass (same costs as the host builders: triangle 1, node step
+// 0.7) then marks the subtrees of <= leaf_size triangles that are cheaper as one leaf; the host lays the
+// tree out depth first (rt_host.cpp build_bvh_ploc). Child boxes get the same conservative padding as the
+// host builders either way, so traversal stays exact.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -157,6 +166,123 @@ __global__ void k_emit_tris(const uint64_t* keys, const TriRec64* rec, TriRec64*
   if (i < n) out[i] = rec[(uint32_t)keys[i]];
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// PLOC
+// ---------------------------------------------------------------------------------------------------
+struct Cluster {
+  Box6 b;
+  int id;  // >= 0: interior node, < 0: ~face (index of the face record)
+  int pad;
+};
+
+__device__ __forceinline__ float half_area(const Box6& b) {
+  const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void k_ploc_init(const uint64_t* keys, const TriRec64* rec, int n, Cluster* cl, Box6* tbox) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = (uint32_t)keys[i];
+  Cluster c;
+  c.b = tri_box(rec[f]);
+  c.id = ~(int)f;
+  c.pad = 0;
+  cl[i] = c;
+  tbox[f] = c.b;
+}
+
+// nearest neighbour of every cluster among the `radius` clusters either side in Morton order (surface
+// area of the merged box; ties to the smaller index, so the pair that is smallest under (area, lower
+// index, higher index) is always mutual and every iteration merges at least once). One block of
+// kPlocBlock clusters stages its window [first - radius, first + kPlocBlock + radius) in LDS.
+constexpr int kPlocBlock = 256, kPlocMaxRadius = 32;
+__global__ __launch_bounds__(kPlocBlock) void k_ploc_nn(const Cluster* cl, int n, int radius, int* nn) {
+  __shared__ Box6 win[kPlocBlock + 2 * kPlocMaxRadius];
+  const int first = (int)blockIdx.x * kPlocBlock;
+  const int lo = first - radius, cnt = kPlocBlock + 2 * radius;
+  for (int k = (int)threadIdx.x; k < cnt; k += kPlocBlock) {
+    const int g = lo + k;
+    if (g >= 0 && g < n) win[k] = cl[g].b;
+  }
+  __syncthreads();
+  const int i = first + (int)threadIdx.x;
+  if (i >= n) return;
+  const Box6 bi = win[i - lo];
+  float best = INFINITY;
+  int bj = -1;
+  const int j0 = max(0, i - radius), j1 = min(n - 1, i + radius);
+  for (int j = j0; j <= j1; j++) {
+    if (j == i) continue;
+    const float d = half_area(join(bi, win[j - lo]));
+    if (d < best) { best = d; bj = j; }  // ascending j: the first minimum is the smaller index
+  }
+  nn[i] = bj;
+}
+
+// per cluster: merge flag (the lower index of a mutual pair) in the high word, keep flag (not the higher
+// index of a mutual pair) in the low word -- one exclusive scan gives both output positions
+__global__ void k_ploc_flags(const int* nn, int n, uint64_t* flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int j = nn[i];
+  const bool mutual = j >= 0 && nn[j] == i;
+  const uint64_t merge = (mutual && i < j) ? 1u : 0u, keep = (mutual && j < i) ? 0u : 1u;
+  flags[i] = (merge << 32) | keep;
+}
+
+// the merged clusters become interior nodes node_base + (their merge rank); the survivors move to their
+// compacted position (Morton order kept)
+__global__ void k_ploc_merge(const Cluster* cl, const int* nn, const uint64_t* flags, const uint64_t* pos, int n,
+                             int node_base, Cluster* out, int2* child, Box6* nbox, int* parent_int, int* parent_leaf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t f = flags[i];
+  if (!(f & 0xFFFFFFFFull)) return;  // merged into its lower-index partner
+  Cluster c = cl[i];
+  if (f >> 32) {
+    const int node = node_base + (int)(pos[i] >> 32);
+    const Cluster o = cl[nn[i]];
+    child[node] = make_int2(c.id, o.id);
+    if (c.id >= 0) parent_int[c.id] = node; else parent_leaf[~c.id] = node;
+    if (o.id >= 0) parent_int[o.id] = node; else parent_leaf[~o.id] = node;
+    c.b = join(c.b, o.b);
+    nbox[node] = c.b;
+    c.id = node;
+  }
+  out[(uint32_t)pos[i]] = c;
+}
+
+// bottom-up SAH collapse of the finished tree (one thread per face, the second child to finish computes
+// its parent, agent-scope acquire/release as k_bottom_up): per node its triangle count and cost, and
+// `leaf` = the subtree becomes one leaf (<= leaf_size triangles and no costlier than the split). Costs in
+// units of one triangle test: a leaf n * A, an interior node k_trav * A + C(child 0) + C(child 1), A the
+// node's (half) surface area -- the host builders' cost model (triangle 1, node step 0.7).
+__global__ void k_ploc_collapse(const int2* child, const int* parent_int, const int* parent_leaf, const Box6* nbox,
+                                const Box6* tbox, int* flags, int* count, float* cost, uint8_t* leaf, int n,
+                                int leaf_size, float k_trav) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  int node = parent_leaf[k];
+  while (node >= 0) {
+    const int arrived = __hip_atomic_fetch_add(&flags[node], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == 0) return;  // the sibling subtree is not done: it continues from here
+    const int2 c = child[node];
+    const int na = c.x >= 0 ? count[c.x] : 1, nb = c.y >= 0 ? count[c.y] : 1;
+    const float ca = c.x >= 0 ? cost[c.x] : half_area(tbox[~c.x]);
+    const float cb = c.y >= 0 ? cost[c.y] : half_area(tbox[~c.y]);
+    const float A = half_area(nbox[node]);
+    const int m = na + nb;
+    const float split = k_trav * A + ca + cb, as_leaf = (float)m * A;
+    const bool lf = m <= leaf_size && as_leaf <= split;
+    count[node] = m;
+    cost[node] = lf ? as_leaf : split;
+    leaf[node] = lf ? 1 : 0;
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    node = parent_int[node];
+  }
+}
 }  // namespace
 
 // face_recs: one TriRec64 per face in face order. Outputs interior nodes in Karras order (root 0; nodes
@@ -235,6 +361,123 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return RT_OK;
+}
+
+// PLOC (see the top of the file). face_recs: one TriRec64 per face. Outputs the n - 1 interior nodes
+// (root n - 2): children (>= 0 interior node, < 0 ~face), boxes, the SAH collapse flag per node; the
+// host lays the tree out (rt_host.cpp build_bvh_ploc). RT_ERR_INVALID when the clustering cannot finish
+// (an iteration without a merge: non-finite boxes), so the caller builds on the host instead.
+int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
+                   int leaf_size, int radius, float k_trav, std::vector<int32_t>& child2, std::vector<float>& box6,
+                   std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations) {
+  const int n = (int)face_recs.size();
+  if (n < 2) { set_error("gpu_build_ploc: needs at least 2 triangles"); return RT_ERR_INVALID; }
+  radius = std::max(1, std::min(radius, kPlocMaxRadius));
+  BCHECK(hipSetDevice(device));
+  hipStream_t st;
+  BCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  struct Guard {
+    hipStream_t st;
+    std::vector<void*> bufs;
+    ~Guard() {
+      (void)hipStreamSynchronize(st);
+      for (void* b : bufs) (void)hipFree(b);
+      (void)hipStreamDestroy(st);
+    }
+  } g{st, {}};
+  auto alloc = [&](void** p, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+    if (e == hipSuccess) g.bufs.push_back(*p);
+    return e;
+  };
+  TriRec64* d_rec = nullptr;
+  uint64_t *d_k0 = nullptr, *d_k1 = nullptr, *d_flags = nullptr, *d_pos = nullptr;
+  Cluster *d_ca = nullptr, *d_cb = nullptr;
+  Box6 *d_tbox = nullptr, *d_nbox = nullptr;
+  int2* d_child = nullptr;
+  int *d_nn = nullptr, *d_pint = nullptr, *d_pleaf = nullptr, *d_cflags = nullptr, *d_count = nullptr;
+  float* d_cost = nullptr;
+  uint8_t* d_leaf = nullptr;
+  BCHECK(alloc((void**)&d_rec, (size_t)n * sizeof(TriRec64)));
+  BCHECK(alloc((void**)&d_k0, (size_t)n * 8));
+  BCHECK(alloc((void**)&d_k1, (size_t)n * 8));
+  BCHECK(alloc((void**)&d_flags, (size_t)n * 8));
+  BCHECK(alloc((void**)&d_pos, (size_t)n * 8));
+  BCHECK(alloc((void**)&d_ca, (size_t)n * sizeof(Cluster)));
+  BCHECK(alloc((void**)&d_cb, (size_t)n * sizeof(Cluster)));
+  BCHECK(alloc((void**)&d_tbox, (size_t)n * sizeof(Box6)));
+  BCHECK(alloc((void**)&d_nbox, (size_t)n * sizeof(Box6)));
+  BCHECK(alloc((void**)&d_child, (size_t)n * sizeof(int2)));
+  BCHECK(alloc((void**)&d_nn, (size_t)n * 4));
+  BCHECK(alloc((void**)&d_pint, (size_t)n * 4));
+  BCHECK(alloc((void**)&d_pleaf, (size_t)n * 4));
+  BCHECK(alloc((void**)&d_cflags, (size_t)n * 4));
+  BCHECK(alloc((void**)&d_count, (size_t)n * 4));
+  BCHECK(alloc((void**)&d_cost, (size_t)n * 4));
+  BCHECK(alloc((void**)&d_leaf, (size_t)n));
+  BCHECK(hipMemcpyAsync(d_rec, face_recs.data(), (size_t)n * sizeof(TriRec64), hipMemcpyHostToDevice, st));
+  BCHECK(hipMemsetAsync(d_pint, 0xFF, (size_t)n * 4, st));  // the root's parent: -1
+  BCHECK(hipMemsetAsync(d_cflags, 0, (size_t)n * 4, st));
+  hipEvent_t e0, e1;
+  BCHECK(hipEventCreate(&e0));
+  BCHECK(hipEventCreate(&e1));
+  BCHECK(hipEventRecord(e0, st));
+  const int B = 256, G = (n + B - 1) / B;
+  float3 flo = make_float3(lo[0], lo[1], lo[2]), fsc;
+  fsc.x = hi[0] > lo[0] ? 1024.0f / (hi[0] - lo[0]) : 0.0f;
+  fsc.y = hi[1] > lo[1] ? 1024.0f / (hi[1] - lo[1]) : 0.0f;
+  fsc.z = hi[2] > lo[2] ? 1024.0f / (hi[2] - lo[2]) : 0.0f;
+  hipLaunchKernelGGL(k_morton, dim3(G), dim3(B), 0, st, (const TriRec64*)d_rec, n, flo, fsc, d_k0);
+  size_t tb = 0, tscan = 0;
+  BCHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_k0, d_k1, n, 0, 64, st));
+  BCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, d_flags, d_pos, n, st));
+  void* d_tmp = nullptr;
+  BCHECK(alloc(&d_tmp, std::max(tb, tscan)));
+  BCHECK(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb, d_k0, d_k1, n, 0, 64, st));
+  hipLaunchKernelGGL(k_ploc_init, dim3(G), dim3(B), 0, st, (const uint64_t*)d_k1, (const TriRec64*)d_rec, n, d_ca, d_tbox);
+  BCHECK(hipGetLastError());
+  int N = n, base = 0, iters = 0;
+  Cluster *cur = d_ca, *nxt = d_cb;
+  while (N > 1) {
+    const int g = (N + kPlocBlock - 1) / kPlocBlock;
+    hipLaunchKernelGGL(k_ploc_nn, dim3(g), dim3(kPlocBlock), 0, st, (const Cluster*)cur, N, radius, d_nn);
+    hipLaunchKernelGGL(k_ploc_flags, dim3(g), dim3(kPlocBlock), 0, st, (const int*)d_nn, N, d_flags);
+    BCHECK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tscan, d_flags, d_pos, N, st));
+    hipLaunchKernelGGL(k_ploc_merge, dim3(g), dim3(kPlocBlock), 0, st, (const Cluster*)cur, (const int*)d_nn,
+                       (const uint64_t*)d_flags, (const uint64_t*)d_pos, N, base, nxt, d_child, d_nbox, d_pint, d_pleaf);
+    BCHECK(hipGetLastError());
+    uint64_t tail[2];
+    BCHECK(hipMemcpyAsync(&tail[0], d_pos + (N - 1), 8, hipMemcpyDeviceToHost, st));
+    BCHECK(hipMemcpyAsync(&tail[1], d_flags + (N - 1), 8, hipMemcpyDeviceToHost, st));
+    BCHECK(hipStreamSynchronize(st));
+    const uint64_t tot = tail[0] + tail[1];
+    const int merges = (int)(tot >> 32), keeps = (int)(tot & 0xFFFFFFFFull);
+    if (merges == 0 || keeps != N - merges) { set_error("gpu_build_ploc: clustering stalled (non-finite boxes?)"); return RT_ERR_INVALID; }
+    base += merges;
+    N = keeps;
+    std::swap(cur, nxt);
+    iters++;
+  }
+  if (base != n - 1) { set_error("gpu_build_ploc: %d interior nodes for %d faces", base, n); return RT_ERR_INVALID; }
+  hipLaunchKernelGGL(k_ploc_collapse, dim3(G), dim3(B), 0, st, (const int2*)d_child, (const int*)d_pint,
+                     (const int*)d_pleaf, (const Box6*)d_nbox, (const Box6*)d_tbox, d_cflags, d_count, d_cost, d_leaf, n,
+                     std::max(1, std::min(leaf_size, kMaxLeaf)), k_trav);
+  BCHECK(hipGetLastError());
+  BCHECK(hipEventRecord(e1, st));
+  child2.resize(2 * (size_t)(n - 1));
+  box6.resize(6 * (size_t)(n - 1));
+  leaf.resize((size_t)(n - 1));
+  BCHECK(hipMemcpyAsync(child2.data(), d_child, (size_t)(n - 1) * sizeof(int2), hipMemcpyDeviceToHost, st));
+  BCHECK(hipMemcpyAsync(box6.data(), d_nbox, (size_t)(n - 1) * sizeof(Box6), hipMemcpyDeviceToHost, st));
+  BCHECK(hipMemcpyAsync(leaf.data(), d_leaf, (size_t)(n - 1), hipMemcpyDeviceToHost, st));
+  BCHECK(hipStreamSynchronize(st));
+  float ms = 0.0f;
+  BCHECK(hipEventElapsedTime(&ms, e0, e1));
+  if (gpu_ms) *gpu_ms = ms;
+  if (iterations) *iterations = iters;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return RT_OK;

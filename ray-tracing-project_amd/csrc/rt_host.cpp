@@ -1657,6 +1657,95 @@ bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   return true;
 }
 
+// GPU PLOC (rt_build.hip gpu_build_ploc) + host layout: the device returns the clustered binary tree
+// (n - 1 interior nodes, root n - 2) with the SAH collapse flags; here its kept interior nodes get
+// pre-order indices, every collapsed subtree / single triangle becomes a leaf whose triangles take
+// consecutive slots in depth-first order (child 0 first), and relayout_dfs re-lays out the nodes as for the
+// host builders. false (nothing changed) when the device build is impossible or the tree too deep.
+constexpr int kPlocRadius = 24;       // clusters searched either side (the paper's quality setting ~25)
+constexpr float kPlocTrav = 0.7f;     // node-step cost relative to a triangle test (as the host builders)
+bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
+  if (hs.nf < 2) return false;
+  float lo[3], hi[3];
+  world_bounds(hs, lo, hi);
+  std::vector<TriRec64> recs;
+  face_records(hs, recs);
+  std::vector<int32_t> child;
+  std::vector<float> box;
+  std::vector<uint8_t> leaf;
+  int iters = 0;
+  const int lb = std::max(1, std::min(leaf_size, kMaxLeaf));
+  if (gpu_build_ploc(device, recs, lo, hi, lb, kPlocRadius, kPlocTrav, child, box, leaf, gpu_ms, &iters) != RT_OK)
+    return false;
+  const int n = hs.nf, ni = n - 1, root = n - 2;
+  const float pad = bvh_pad(lo, hi);
+  // pre-order walk (child 0 first): kept interior nodes get tmp indices, leaves get their slots
+  std::vector<uint32_t> handle_int((size_t)ni, 0), handle_tri((size_t)n, 0);
+  std::vector<int32_t> kept;  // tmp index -> PLOC node
+  std::vector<TriRec64> tris;
+  tris.reserve((size_t)n);
+  std::vector<int32_t> st{root}, sub;
+  auto tri_of = [&](int32_t c) { return (uint32_t)~c; };
+  while (!st.empty()) {
+    const int32_t c = st.back();
+    st.pop_back();
+    if (c < 0) {  // a single-triangle leaf
+      handle_tri[tri_of(c)] = make_leaf((uint32_t)tris.size(), 1u);
+      tris.push_back(recs[tri_of(c)]);
+    } else if (leaf[(size_t)c] && c != root) {  // a collapsed subtree: its triangles in depth-first order
+      const uint32_t first = (uint32_t)tris.size();
+      sub.assign(1, c);
+      while (!sub.empty()) {
+        const int32_t q = sub.back();
+        sub.pop_back();
+        if (q < 0) { tris.push_back(recs[tri_of(q)]); continue; }
+        sub.push_back(child[2 * (size_t)q + 1]);
+        sub.push_back(child[2 * (size_t)q]);
+      }
+      handle_int[(size_t)c] = make_leaf(first, (uint32_t)tris.size() - first);
+    } else {
+      handle_int[(size_t)c] = (uint32_t)kept.size();
+      kept.push_back(c);
+      st.push_back(child[2 * (size_t)c + 1]);
+      st.push_back(child[2 * (size_t)c]);
+    }
+  }
+  std::vector<Node64> tmp(kept.size());
+  for (size_t k = 0; k < kept.size(); k++) {
+    const int32_t q = kept[k];
+    Node64 nd{};
+    for (int side = 0; side < 2; side++) {
+      const int32_t c = child[2 * (size_t)q + side];
+      float b[6];
+      uint32_t h;
+      if (c < 0) {
+        const TriRec64& t = recs[tri_of(c)];
+        b[0] = std::min(std::min(t.w0x, t.w1x), t.w2x); b[3] = std::max(std::max(t.w0x, t.w1x), t.w2x);
+        b[1] = std::min(std::min(t.w0y, t.w1y), t.w2y); b[4] = std::max(std::max(t.w0y, t.w1y), t.w2y);
+        b[2] = std::min(std::min(t.w0z, t.w1z), t.w2z); b[5] = std::max(std::max(t.w0z, t.w1z), t.w2z);
+        h = handle_tri[tri_of(c)];
+      } else {
+        for (int j = 0; j < 6; j++) b[j] = box[6 * (size_t)c + j];
+        h = handle_int[(size_t)c];
+      }
+      float* o = side ? &nd.c1lx : &nd.c0lx;  // lx hx ly hy lz hz
+      o[0] = b[0] - pad; o[1] = b[3] + pad; o[2] = b[1] - pad; o[3] = b[4] + pad; o[4] = b[2] - pad; o[5] = b[5] + pad;
+      (side ? nd.child1 : nd.child0) = h;
+    }
+    tmp[k] = nd;
+  }
+  HostScene trial;
+  relayout_dfs(trial, tmp, 0);
+  if (trial.depth > kMaxDepth + 2) return false;  // too deep for the wave stack: host SAH instead
+  if (debug_env("RT_TIMING")) fprintf(stderr, "[rt] ploc: %d iterations, %zu nodes, depth %d\n", iters, tmp.size(), trial.depth);
+  hs.nodes = std::move(trial.nodes);
+  hs.root = 0;
+  hs.depth = trial.depth;
+  hs.leaves = trial.leaves;
+  hs.tris = std::move(tris);
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // 4-wide collapse: each wide node takes a binary node's two children and keeps opening the interior
 // child with the largest surface area until it has four children (or only leaves remain). Child
@@ -1942,6 +2031,12 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
             s->box_builder_used == RT_BOXES_GPU ? "gpu" : "host", s->boxes_gpu_ms, hs.boxes.size());
   auto t2 = clk::now();
   bool built = false;
+  if (s->opts.builder == RT_BUILDER_PLOC_GPU && s->opts.device != RT_DEVICE_NONE) {
+    int dev = s->opts.device;
+    if (dev < 0) dev = rt::current_device();
+    built = dev >= 0 && rt::build_bvh_ploc(hs, dev, leaf, &s->bvh_gpu_ms);
+    if (built) s->builder_used = RT_BUILDER_PLOC_GPU;
+  }
   if (s->opts.builder == RT_BUILDER_LBVH_GPU && s->opts.device != RT_DEVICE_NONE) {
     int dev = s->opts.device;
     if (dev < 0) dev = rt::current_device();

@@ -66,6 +66,10 @@ int gpu_build_ref_boxes(int device, HostScene& hs, const float* v4, int32_t min_
 void assign_box_ranks(HostScene& hs);
 void build_bvh(HostScene& hs, int leaf_size, bool spatial);  // spatial: SBVH (RT_BUILDER_SBVH)
 bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms);
+bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms);
+int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
+                   int leaf_size, int radius, float k_trav, std::vector<int32_t>& child2, std::vector<float>& box6,
+                   std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
 void build_bvh4(HostScene& hs);

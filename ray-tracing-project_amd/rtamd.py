@@ -284,7 +284,7 @@ class Mesh:
             self.h = None
 
 
-RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH = 0, 1, 2
+RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH, RT_BUILDER_PLOC_GPU = 0, 1, 2, 3
 RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 

@@ -401,6 +401,33 @@ def test_gpu_lbvh_builder(rt, soup, name):
             assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (name, m)
 
 
+@pytest.mark.parametrize("name", ["bunny", "soup"])
+def test_gpu_ploc_builder(rt, soup, name):
+    """f2 "LBVH/PLOC": the device PLOC build (rt_build.hip) gives a sound tree -- every triangle inside every
+    ancestor box, every face in exactly one leaf, leaves of at most 4 triangles -- and the frame of the
+    host-SBVH scene bit for bit (PRIMARY and FULL)."""
+    if name == "bunny":
+        mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
+        ref = rt.Scene(mesh)
+        W, H = 1920, 1080
+    else:
+        ref, _ = soup
+        mesh = ref.mesh
+        W, H = 960, 540
+    pl = rt.Scene(mesh, builder=rt.RT_BUILDER_PLOC_GPU)
+    info = pl.info()
+    assert info["builder"] == rt.RT_BUILDER_PLOC_GPU and info["bvh_gpu_ms"] > 0
+    assert info["bvh_depth"] <= 62
+    v = pl.validate_bvh()
+    assert v["ok"] and v["covered2"] == info["n_faces"], v
+    cam = rt.flycam(W, H, 0, 0, 20)
+    for m in (rt.RT_MODE_PRIMARY, rt.RT_MODE_FULL):
+        a = ref.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        b = pl.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (name, m)
+
+
 def test_trace_color_and_debug_ray(rt, orc):
     """f4 single-ray queries: traceRay colours of camera rays equal the FULL frame's pixels bit for bit;
     the debug ray's first segment is that pixel's ray, colour and hit distance, and each reflection
