@@ -219,13 +219,14 @@ def gather_all(dist, dev, x):
     return [float(v) for v in out.tolist()]
 
 
-def same_build_profile(W, H, n_faces, mode, kernel, src_hash):
-    """The committed rocprofv3 summary (profiles/pmc_latest.json, tools/profile.sh +
-    tools/summarize_profile.py) when it was taken of this build (embedded source hash), this kernel and
-    this workload, one frame on the GPU at a time; else None."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def same_build_profile(W, H, n_faces, mode, kernel, src_hash, latest="pmc_latest.json"):
+    """The committed rocprofv3 summary (profiles/pmc_latest.json for the headline workload,
+    profiles/pmc_latest_c5.json for C5; tools/profile.sh + tools/summarize_profile.py) when it was taken of
+    this build (embedded source hash), this kernel and this workload, one frame on the GPU at a time; else
+    None."""
+    p = os.path.join(ROOT, "profiles", latest)
     if not os.path.exists(p):
-        return None, "no profiles/pmc_latest.json"
+        return None, f"no profiles/{latest}"
     d = json.load(open(p))
     bl = d.get("bench_line_under_trace", {})
     cfg = bl.get("config", {})
@@ -237,7 +238,7 @@ def same_build_profile(W, H, n_faces, mode, kernel, src_hash):
     if bl.get("build", {}).get("source_hash") != src_hash:
         why.append(f"other build ({bl.get('build', {}).get('source_hash')} vs {src_hash})")
     if why:
-        return None, f"profiles/pmc_latest.json ({d.get('tag')}): " + ", ".join(why)
+        return None, f"profiles/{latest} ({d.get('tag')}): " + ", ".join(why)
     return d, f"profiles/{d.get('tag')}_pmc.json"
 
 
@@ -314,7 +315,51 @@ def frame_parity(rt, sc, W, H, mode, case):
     return out
 
 
-def side_config(rt, scene_name, mode, steps, warmup, device):
+def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash, mode_name, latest, split=False,
+                shard=(0, 1)):
+    """The dominant kernel's packet-byte roofline for one workload (see the module docstring): a counting run
+    of the same frame for the bytes, the isolated launch duration kern_ms, the same build's profile (if
+    committed) for the measured HBM traffic and the limiter."""
+    sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard, flags=rt.RT_FRAME_STATS)
+    stats = sc.synchronize()
+    rays = max(stats["primary_rays"], 1)
+    n_node = stats["node_visits"] / rays
+    n_tri = stats["tri_tests"] / rays
+    hit = stats["hits"] / rays
+    kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
+    # the packet algorithm's bytes per launch: node / triangle records once per wave, the hit lanes'
+    # triangle + shading records, the pixel
+    wave_bytes = float(stats["wave_node_bytes"]) + 64.0 * stats["wave_tri_fetches"]
+    alg_bytes = wave_bytes + stats["hits"] * (64 + 48) + 12.0 * rays
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    prof, prof_src = same_build_profile(W, H, n_faces, mode_name, kname, src_hash, latest)
+    traffic = traffic_b = issue = limiter = None
+    if prof is not None:
+        traffic_b = prof.get("hbm_bytes_per_launch")
+        if traffic_b:
+            traffic = round(traffic_b / (kern_ms * 1e-3) / 1e9, 1)
+        issue = prof.get("issue")
+        limiter = prof.get("limiter")
+    # what bounds the kernel, as the newest committed profile of it measured (VERDICT r2 item 3): the
+    # roofline below is still priced against HBM bandwidth, the resource north_star names
+    bound, bound_src = kernel_bound(kname)
+    roof = {"bound": bound, "bound_source": bound_src, "priced_against": "hbm",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "traffic_bytes_per_launch": traffic_b, "traffic_source": prof_src,
+            "kernel": kname, "kernel_ms_isolated": round(kern_ms, 4),
+            "algorithmic_bytes_per_launch": int(alg_bytes),
+            "algorithmic_bytes_per_ray": round(alg_bytes / rays, 1),
+            "per_step_GBps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            "limiter": limiter, "issue": issue,
+            # SURVEY 8(d) d3's per-ray demand (every node / triangle a ray visits, as if each ray read
+            # its own records): served from SGPRs / L2 / MALL, not HBM -- reported, not priced
+            "survey_demand_bytes_per_ray": round(64 * n_node + 40 * n_tri + 92 * hit + 12, 1),
+            "n_node": round(n_node, 2), "n_tri": round(n_tri, 2), "hit": round(hit, 4)}
+    return roof, stats
+
+
+def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None):
     """A single-GPU BASELINE config beside the headline one: C2 = bunny PRIMARY,
     C5 = bunny FULL, 1920x1080: rate with frames in flight and one frame at a time."""
     W, H = 1920, 1080
@@ -329,8 +374,13 @@ def side_config(rt, scene_name, mode, steps, warmup, device):
         out["mrays_per_s" + key] = round(st["primary_rays"] * steps / el / 1e6, 2)
         out["ms_per_frame" + key] = round(el / steps * 1e3, 4)
         if fif == 4:
-            sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, flags=rt.RT_FRAME_STATS)
-            s2 = sc.synchronize()
+            # the frame's kernel alone on the GPU (HIP events, 20 frames each synchronised before the next)
+            iso, _ = isolated_kernel_ms(rt, sc, cam, W, H, m, (0, 1))
+            out["kernel_ms_isolated"] = round(iso, 4)
+            roof, s2 = roofline_of(rt, sc, cam, W, H, m, iso, el / steps * 1e3, sc.info()["n_faces"], src_hash, mode,
+                                   "pmc_latest_c5.json" if mode == "full" else "pmc_latest_c2.json")
+            out["roofline"] = roof
+            out["limiter"] = roof["limiter"]
             out["total_mrays_per_s"] = round(s2["total_rays"] * steps / el / 1e6, 2)
             out["parity"] = frame_parity(rt, sc, W, H, m, scene_name)
         del sc
@@ -507,50 +557,15 @@ def main():
     side = {}
     if n == 1 and not a.no_side and a.frame is None and a.scene == "soup" and a.mode == "primary" and not K:
         for cn, md in (("c2", "primary"), ("c5", "full")):
-            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local)
+            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local, ident["source_hash"])
 
     roof = None
     stats = None
     if rank == 0 and not a.no_stats:
-        # counting run of the same kernels on the same frame (RT_FRAME_STATS)
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard, flags=rt.RT_FRAME_STATS)
-        stats = sc.synchronize()
-        rays = max(stats["primary_rays"], 1)
-        n_node = stats["node_visits"] / rays
-        n_tri = stats["tri_tests"] / rays
-        hit = stats["hits"] / rays
         split = mode == rt.RT_MODE_PRIMARY and os.environ.get("RTAMD_DEBUG_KNOBS") == "1" and (int(os.environ.get("RT_KERNEL_VARIANT", "0") or 0) & (32768 | 256 | 2048))
-        kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
-        # the packet algorithm's bytes per launch: node / triangle records once per wave, the hit lanes'
-        # triangle + shading records, the pixel
-        wave_bytes = float(stats["wave_node_bytes"]) + 64.0 * stats["wave_tri_fetches"]
-        alg_bytes = wave_bytes + stats["hits"] * (64 + 48) + 12.0 * rays
         kern_ms = iso_trace_ms if mode == rt.RT_MODE_PRIMARY else iso_ms
-        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        prof, prof_src = same_build_profile(W, H, info["n_faces"], a.mode, kname, ident["source_hash"])
-        traffic = traffic_b = issue = limiter = None
-        if prof is not None:
-            traffic_b = prof.get("hbm_bytes_per_launch")
-            if traffic_b:
-                traffic = round(traffic_b / (kern_ms * 1e-3) / 1e9, 1)
-            issue = prof.get("issue")
-            limiter = prof.get("limiter")
-        # what bounds the kernel, as the newest committed profile of it measured: the
-        # roofline below is still priced against HBM bandwidth, the resource north_star names
-        bound, bound_src = kernel_bound(kname)
-        roof = {"bound": bound, "bound_source": bound_src, "priced_against": "hbm",
-                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "traffic_bytes_per_launch": traffic_b, "traffic_source": prof_src,
-                "kernel": kname, "kernel_ms_isolated": round(kern_ms, 4),
-                "algorithmic_bytes_per_launch": int(alg_bytes),
-                "algorithmic_bytes_per_ray": round(alg_bytes / rays, 1),
-                "per_step_GBps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                "limiter": limiter, "issue": issue,
-                # SURVEY 8(d) d3's per-ray demand (every node / triangle a ray visits, as if each ray read
-                # its own records): served from SGPRs / L2 / MALL, not HBM -- reported, not priced
-                "survey_demand_bytes_per_ray": round(64 * n_node + 40 * n_tri + 92 * hit + 12, 1),
-                "n_node": round(n_node, 2), "n_tri": round(n_tri, 2), "hit": round(hit, 4)}
+        roof, stats = roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, info["n_faces"], ident["source_hash"],
+                                  a.mode, "pmc_latest.json", split, shard)
 
     # the headline frame's parity against the committed oracle digests (every pixel; N = 1, C3)
     headline_parity = None

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-4 GPU pass: GPU tests, the default bench line, then rocprofv3 profiles of the headline kernel (C3)
+# and of the C5 FULL kernel (bench sub-line limiter). Every GPU step has its own time limit; stop at the
+# first hard failure. Usage: bash tools/gpu_round4.sh <tag> [tests bench prof profc5 ...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests bench prof profc5}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+hard() { case $1 in 124|134|137|139) echo "hard failure ($1): stopping"; exit $1;; esac; }
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread \
+          --durations=15 > $OUT/pytest_gpu.log 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -25 $OUT/pytest_gpu.log; hard $rc ;;
+    bench)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err
+      rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; hard $rc; [ $rc -ne 0 ] && exit $rc ;;
+    ploc)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 --builder ploc --no-cpu --no-side > $OUT/bench_ploc.json 2> $OUT/bench_ploc.err
+      rc=$?; echo "ploc rc=$rc"; cat $OUT/bench_ploc.json; hard $rc ;;
+    prof)
+      OUTDIR=$OUT/prof bash tools/profile.sh > $OUT/profile.log 2>&1
+      rc=$?; echo "profile rc=$rc"; tail -12 $OUT/profile.log; hard $rc ;;
+    profc5)
+      OUTDIR=$OUT/profc5 \
+      BENCH_ARGS="--scene bunny --mode full --steps 20 --warmup 3 --no-cpu --no-extra --no-e2e --no-side --frames-in-flight 1" \
+      PMC_ARGS="--scene bunny --mode full --steps 5 --warmup 1 --no-cpu --no-stats --no-extra --no-e2e --no-side --frames-in-flight 1" \
+      bash tools/profile.sh > $OUT/profile_c5.log 2>&1
+      rc=$?; echo "profile c5 rc=$rc"; tail -12 $OUT/profile_c5.log; hard $rc ;;
+  esac
+done
+exit 0

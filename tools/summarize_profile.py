@@ -115,8 +115,12 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
     out["tag"] = tag
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc.json")
     json.dump(out, open(path, "w"), indent=1)
-    if os.environ.get("RT_PROFILE_LATEST", "1") != "0":  # 0: a side profile (not the bench workload's)
-        json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_latest.json"), "w"), indent=1)
+    # RT_PROFILE_LATEST: 1 (default) the headline workload's profile -> pmc_latest.json; c5 / c2 the bench
+    # line's C5 / C2 sub-line profile -> pmc_latest_c5.json / pmc_latest_c2.json; 0 a side profile only
+    latest = os.environ.get("RT_PROFILE_LATEST", "1")
+    if latest != "0":
+        name = "pmc_latest.json" if latest == "1" else f"pmc_latest_{latest}.json"
+        json.dump(out, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "bench_line_under_trace"}, indent=1))
 
 
