@@ -135,7 +135,8 @@ struct Ray {
   f3 o, d;      // world space (triangle tests)
   f3 id;        // culling: 1/d (zeros nudged)
   f3 oa, ob;    // culling: -(o + p)/d and -(o - p)/d, the lo / hi plane offsets of boxes grown by p
-  f3 o2, d2;    // object space (reference intersectBox): Minv*o_box, normalized(MS*d)
+  f3 o2;        // object space (reference intersectBox): Minv*o_box; its direction normalized(MS*d) is
+                // formed where the exact box test needs it (ref_box_test), off the traversal's registers
 };
 
 __device__ __forceinline__ float nudge(float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; }
@@ -228,10 +229,13 @@ __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, f
 constexpr int kFcmpOLE = 5;
 __device__ __forceinline__ uint64_t mask_le(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOLE); }
 
-// The reference's object-space box test, exact (flyscene.cpp:484-507)
-__device__ __forceinline__ bool ref_box_test(const Ray& r, const float* bx) {
+// The reference's object-space box test, exact (flyscene.cpp:484-507): origin Minv*o (Ray::o2), direction
+// (MS*d).normalized() with MS the linear block of Minv (flyscene.cpp:486-487; m3v3's Matrix3f order)
+__device__ __forceinline__ bool ref_box_test(const DevScene& S, const Ray& r, const float* bx) {
+  const float MS[9] = {S.Minv[0], S.Minv[1], S.Minv[2], S.Minv[4], S.Minv[5], S.Minv[6], S.Minv[8], S.Minv[9], S.Minv[10]};
+  const f3 dd = normalized(m3v3(MS, r.d));
   const float lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[4], bx[5], bx[6]};
-  const float o2[3] = {r.o2.x, r.o2.y, r.o2.z}, d2[3] = {r.d2.x, r.d2.y, r.d2.z};
+  const float o2[3] = {r.o2.x, r.o2.y, r.o2.z}, d2[3] = {dd.x, dd.y, dd.z};
   float tin3[3], tout3[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -287,7 +291,7 @@ __device__ __forceinline__ uint64_t accept_candidate(const DevScene& P, const Tr
   }
   const uint64_t ins = ballot(inside);
   if ((cand & ~ins) == 0) return cand;
-  return cand & (ins | ballot(ref_box_test(r, bx)));
+  return cand & (ins | ballot(ref_box_test(P, r, bx)));
 }
 
 // calculateDistance (flyscene.cpp:444-478) against a wave-uniform triangle record, for the lanes of
@@ -1114,7 +1118,6 @@ __device__ __forceinline__ f3 calc_color(const FrameParams& P, MatState& st, con
       sr.o = offset(hi.p, L, 0.003f);
       sr.d = L;
       sr.o2 = affv3(P.Minv, hi.p);
-      sr.d2 = normalized(m3v3(P.MS, L));
       setup_cull(sr, P.sc.static_pad);
       Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if (STATS && lane_hit) cnt[ST_TOTAL]++;
@@ -1215,7 +1218,6 @@ __device__ __forceinline__ Ray primary_ray(const FrameParams& P, int px, int py)
   r.o = f3{P.eye[0], P.eye[1], P.eye[2]};
   r.d = normalized(sub(w, r.o));
   r.o2 = f3{P.eye_obj[0], P.eye_obj[1], P.eye_obj[2]};
-  r.d2 = normalized(m3v3(P.MS, r.d));
   setup_cull(r, P.sc.static_pad);
   return r;
 }
@@ -1415,7 +1417,6 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   rr.d = reflect(normalized(r.d), hi0.n);
   rr.o = offset(hi0.p, rr.d, 0.001f);
   rr.o2 = affv3(P.Minv, rr.o);
-  rr.d2 = normalized(m3v3(P.MS, rr.d));
   setup_cull(rr, P.sc.static_pad);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -1553,7 +1554,6 @@ void k_render_depth(FrameParams P) {
     rr.d = reflect(normalized(cur.d), hi.n);
     rr.o = offset(hi.p, rr.d, 0.001f);
     rr.o2 = affv3(P.Minv, rr.o);
-    rr.d2 = normalized(m3v3(P.MS, rr.d));
     setup_cull(rr, P.sc.static_pad);
     if (STATS && hit) cnt[ST_TOTAL]++;
     cur = rr;
@@ -1600,7 +1600,6 @@ __global__ __launch_bounds__(256) void k_rays(FrameParams P, RayParams R) {
     r.d = ld3(R.d + 3 * (size_t)j);
     r.o2 = affv3(P.Minv, r.o);
   }
-  r.d2 = normalized(m3v3(P.MS, r.d));
   setup_cull(r, P.sc.static_pad);
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool found = false;
@@ -1648,7 +1647,6 @@ void k_rays_color(FrameParams P, RayParams R) {
   r.o = ld3(R.o + 3 * (size_t)j);
   r.d = ld3(R.d + 3 * (size_t)j);
   r.o2 = affv3(P.Minv, r.o);
-  r.d2 = normalized(m3v3(P.MS, r.d));
   setup_cull(r, P.sc.static_pad);
   Hit h;
   uint32_t face0;

@@ -316,7 +316,7 @@ __device__ __forceinline__ bool accept_lane(const DevScene& P, const TriRec64& t
     const float m = 1e-5f * ((hi[k] - lo[k]) + fabsf(lo[k]) + fabsf(hi[k]) + fabsf(os[k])) + 1e-30f;
     inside = inside & (xs[k] > lo[k] + m) & (xs[k] < hi[k] - m);
   }
-  return inside || ref_box_test(r, bx);
+  return inside || ref_box_test(P, r, bx);
 }
 
 // calculateDistance (flyscene.cpp:444-478) of one lane against its own triangle record
@@ -682,7 +682,6 @@ void k_full_shadow(FrameParams P, int pass) {
     sr.o = offset(p, Ld, 0.003f);
     sr.d = Ld;
     sr.o2 = affv3(P.Minv, p);
-    sr.d2 = normalized(m3v3(P.MS, Ld));
     setup_cull(sr, P.sc.static_pad);
     Hit hh{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
     bool blocked = false;
@@ -712,7 +711,6 @@ void k_full_refl(FrameParams P) {
   rr.d = f3{rq.dx, rq.dy, rq.dz};
   rr.o = f3{rq.ox, rq.oy, rq.oz};
   rr.o2 = affv3(P.Minv, rr.o);
-  rr.d2 = normalized(m3v3(P.MS, rr.d));
   setup_cull(rr, P.sc.static_pad);
   uint32_t cnt[ST_COUNT] = {};
   if (STATS && L.act) cnt[ST_TOTAL]++;
