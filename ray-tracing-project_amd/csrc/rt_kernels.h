@@ -1675,6 +1675,7 @@ enum VariantOp {
   VOP_PRIMARY_X2,         // two rays per lane (variant bit 256)
   VOP_PRIMARY_PERSISTENT, // persistent threads (variant bit 2048; 4096: no stealing)
   VOP_RAYS,               // ray-list queries with a non-default traversal flavour
+  VOP_PRIMARY_FRUSTUM,    // PRIMARY descent by the packet's frustum test (variant bit 4194304)
 };
 struct VariantCall {
   FrameParams P;

@@ -206,7 +206,7 @@ VARIANTS = {"xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-8-w
 # the A/B kernels of the variants library only (rt_variants.hip, `make variants`)
 VARIANTS_LIB = {"vgpr-stack": 1, "wide4": 2, "full-pipeline": 16, "pipeline-lane-refl": 48,
                 "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
-                "persistent-no-steal": 2048 | 4096, "dual-chain": 1048576}
+                "persistent-no-steal": 2048 | 4096, "dual-chain": 1048576, "frustum-descent": 4194304}
 
 
 def variant_frames_identical(rt, scenes, bits):
