@@ -261,7 +261,7 @@ __global__ void k_ploc_merge(const Cluster* cl, const int* nn, const uint64_t* f
 // node's (half) surface area -- the host builders' cost model (triangle 1, node step 0.7).
 __global__ void k_ploc_collapse(const int2* child, const int* parent_int, const int* parent_leaf, const Box6* nbox,
                                 const Box6* tbox, int* flags, int* count, float* cost, uint8_t* leaf, int n,
-                                int leaf_size, float k_trav) {
+                                int leaf_size, float k_trav, int rule) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   int node = parent_leaf[k];
@@ -274,7 +274,10 @@ __global__ void k_ploc_collapse(const int2* child, const int* parent_int, const 
     const float cb = c.y >= 0 ? cost[c.y] : half_area(tbox[~c.y]);
     const float A = half_area(nbox[node]);
     const int m = na + nb;
-    const float split = k_trav * A + ca + cb, as_leaf = (float)m * A;
+    // rule 1 (A/B): the top-down builders' greedy test, children priced as leaves (n_c * A_c)
+    const float pa = rule == 1 && c.x >= 0 ? (float)na * half_area(nbox[c.x]) : ca;
+    const float pb = rule == 1 && c.y >= 0 ? (float)nb * half_area(nbox[c.y]) : cb;
+    const float split = k_trav * A + (m <= leaf_size ? pa + pb : ca + cb), as_leaf = (float)m * A;
     const bool lf = m <= leaf_size && as_leaf <= split;
     count[node] = m;
     cost[node] = lf ? as_leaf : split;
@@ -372,7 +375,7 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
 // (an iteration without a merge: non-finite boxes), so the caller builds on the host instead.
 int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, int radius, float k_trav, std::vector<int32_t>& child2, std::vector<float>& box6,
-                   std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations) {
+                   std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations, int rule) {
   const int n = (int)face_recs.size();
   if (n < 2) { set_error("gpu_build_ploc: needs at least 2 triangles"); return RT_ERR_INVALID; }
   radius = std::max(1, std::min(radius, kPlocMaxRadius));
@@ -464,7 +467,7 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   if (base != n - 1) { set_error("gpu_build_ploc: %d interior nodes for %d faces", base, n); return RT_ERR_INVALID; }
   hipLaunchKernelGGL(k_ploc_collapse, dim3(G), dim3(B), 0, st, (const int2*)d_child, (const int*)d_pint,
                      (const int*)d_pleaf, (const Box6*)d_nbox, (const Box6*)d_tbox, d_cflags, d_count, d_cost, d_leaf, n,
-                     std::max(1, std::min(leaf_size, kMaxLeaf)), k_trav);
+                     std::max(1, std::min(leaf_size, kMaxLeaf)), k_trav, rule);
   BCHECK(hipGetLastError());
   BCHECK(hipEventRecord(e1, st));
   child2.resize(2 * (size_t)(n - 1));

@@ -15,8 +15,10 @@ namespace {
 
 constexpr char kMagic[8] = {'R', 'T', 'S', 'C', 'E', 'N', 'E', '1'};
 // 2: + object-space vertices (RT_MODE_BOX_COLORS); 3: the header's builder field (version-2 files held 0
-// there, which would read as RT_BUILDER_SAH whatever built them, so they are refused and rebuilt)
-constexpr uint32_t kVersion = 3;
+// there, which would read as RT_BUILDER_SAH whatever built them, so they are refused and rebuilt);
+// 4: trees of scenes with tilted face normals bound the accept region (HostScene::av), not the world
+// triangles, so an older file of such a scene could cull hits
+constexpr uint32_t kVersion = 4;
 
 struct Header {
   char magic[8];
@@ -239,6 +241,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
     // the records' flag bits let the kernels skip the normal check and the reference box predicate:
     // recomputed from the loaded geometry, never taken from the file (a crafted file could set them)
     const float Ro = rt::cert_origin_max(hs);
+    rt::accept_region(hs);
     for (rt::TriRec64& t : hs.tris) t.box = (t.box & rt::kBoxIndexMask) | rt::tri_flags(hs, t.face, Ro);
   }
   auto handle_ok = [&](uint32_t c, int32_t n_inner) {

@@ -926,7 +926,7 @@ struct SbvhBuilder {
 
   void verts(uint32_t f, double v[3][3]) const {
     for (int j = 0; j < 3; j++) {
-      const f3& w = hs.wv[hs.fidx[3 * f + j]];
+      const f3& w = bound_vert(hs, f, j);
       v[j][0] = w.x; v[j][1] = w.y; v[j][2] = w.z;
     }
   }
@@ -1251,19 +1251,21 @@ float bvh_pad(const float lo[3], const float hi[3]) {
 // the static pad the builders gave every box: bvh_pad of the triangles' bounds (the builders' `world`)
 float scene_static_pad(const HostScene& hs) {
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (const TriRec64& t : hs.tris) {
-    const float v[9] = {t.w0x, t.w0y, t.w0z, t.w1x, t.w1y, t.w1z, t.w2x, t.w2y, t.w2z};
-    for (int j = 0; j < 3; j++)
-      for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], v[3 * j + k]); hi[k] = std::max(hi[k], v[3 * j + k]); }
-  }
+  for (const TriRec64& t : hs.tris)
+    for (int j = 0; j < 3; j++) {
+      const f3& w = bound_vert(hs, t.face, j);
+      const float v[3] = {w.x, w.y, w.z};
+      for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], v[k]); hi[k] = std::max(hi[k], v[k]); }
+    }
   return hs.tris.empty() ? 0.0f : bvh_pad(lo, hi);
 }
 
 void world_bounds(const HostScene& hs, float lo[3], float hi[3]) {
   Aabb parts[16];
-  const int T = parallel_chunks((size_t)hs.nv, [&](size_t b, size_t e, int t) {
+  const std::vector<f3>& pts = hs.av.empty() ? hs.wv : hs.av;
+  const int T = parallel_chunks(pts.size(), [&](size_t b, size_t e, int t) {
     for (size_t i = b; i < e; i++) {
-      const float c[3] = {hs.wv[i].x, hs.wv[i].y, hs.wv[i].z};
+      const float c[3] = {pts[i].x, pts[i].y, pts[i].z};
       parts[t].growp(c);
     }
   });
@@ -1338,6 +1340,41 @@ static double face_normal_tilt(const HostScene& hs, uint32_t f) {
   return std::sqrt((x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) / (gg * nn));
 }
 
+// The edge tests (flyscene.cpp:580-590) accept P when n.(e_k x (P - w_k)) >= 0 for the three world edges,
+// n the object-space face normal; P = o + t d lies on n's plane n.x = dist (:459-465). Adding multiples of
+// n to e_k or P - w_k leaves those triple products unchanged, so the accepted set is the world triangle
+// projected along n onto that plane, p_k = w_k - ((n.w_k - dist) / n.n) n -- the world triangle itself
+// only when n is its normal. A face whose normal tilts by more than kBoundTilt (offsets above 1e-6 of
+// its diameter, well inside the static pad's rounding allowance) is bounded by that projection; an
+// untilted scene keeps hs.av empty and its builds unchanged. (A normal facing away from the triangle
+// accepts nothing beyond rounding; its projection still bounds that.)
+constexpr double kBoundTilt = 1e-6;
+void accept_region(HostScene& hs) {
+  hs.av.clear();
+  std::atomic<bool> any{false};
+  parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int) {
+    for (size_t f = b; f < e && !any.load(std::memory_order_relaxed); f++)
+      if (!(face_normal_tilt(hs, (uint32_t)f) <= kBoundTilt)) any = true;
+  });
+  if (!any) return;
+  hs.av.resize(3 * (size_t)hs.nf);
+  parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int) {
+    for (size_t f = b; f < e; f++) {
+      const f3& nf = hs.fnn[f];
+      const double n[3] = {nf.x, nf.y, nf.z}, nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+      const bool tilted = !(face_normal_tilt(hs, (uint32_t)f) <= kBoundTilt);
+      for (int j = 0; j < 3; j++) {
+        const f3& w = hs.wv[hs.fidx[3 * f + j]];
+        f3& p = hs.av[3 * f + j];
+        p = w;
+        if (!tilted || !(nn > 0.0) || !std::isfinite(nn)) continue;
+        const double s = (n[0] * w.x + n[1] * w.y + n[2] * w.z - (double)hs.fdist[f]) / nn;
+        p = f3{(float)(w.x - s * n[0]), (float)(w.y - s * n[1]), (float)(w.z - s * n[2])};
+      }
+    }
+  });
+}
+
 static bool box_certified(const HostScene& hs, uint32_t f, float Ro) {
   if (!(Ro > 0.0f) || hs.ov3.empty()) return false;
   const double tilt = face_normal_tilt(hs, f);
@@ -1403,6 +1440,25 @@ void face_records(const HostScene& hs, std::vector<TriRec64>& out) {
   parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int) {
     for (size_t f = b; f < e; f++) tri_record(hs, (uint32_t)f, out[f], Ro);
   });
+}
+
+// the GPU builders bound the records' vertices: with a tilted normal anywhere (hs.av non-empty) they get
+// the accept-region vertices, and world_records puts the world vertices back into the built leaf order
+static void set_verts(TriRec64& r, const f3& w0, const f3& w1, const f3& w2) {
+  r.w0x = w0.x; r.w0y = w0.y; r.w0z = w0.z;
+  r.w1x = w1.x; r.w1y = w1.y; r.w1z = w1.z;
+  r.w2x = w2.x; r.w2y = w2.y; r.w2z = w2.z;
+}
+static void bound_records(const HostScene& hs, std::vector<TriRec64>& recs) {
+  if (hs.av.empty()) return;
+  for (TriRec64& r : recs) set_verts(r, bound_vert(hs, r.face, 0), bound_vert(hs, r.face, 1), bound_vert(hs, r.face, 2));
+}
+static void world_records(HostScene& hs) {
+  if (hs.av.empty()) return;
+  for (TriRec64& r : hs.tris) {
+    const uint32_t* v = &hs.fidx[3 * (size_t)r.face];
+    set_verts(r, hs.wv[v[0]], hs.wv[v[1]], hs.wv[v[2]]);
+  }
 }
 
 // Traversal-order hint of a node for waves whose rays share one direction octant (bit k of the octant:
@@ -1586,7 +1642,7 @@ void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
       p.id = (uint32_t)f;
       for (int k = 0; k < 3; k++) { p.lo[k] = INFINITY; p.hi[k] = -INFINITY; }
       for (int j = 0; j < 3; j++) {
-        const f3& w = hs.wv[hs.fidx[3 * f + j]];
+        const f3& w = bound_vert(hs, (uint32_t)f, j);
         const float c[3] = {w.x, w.y, w.z};
         for (int k = 0; k < 3; k++) { p.lo[k] = std::min(p.lo[k], c[k]); p.hi[k] = std::max(p.hi[k], c[k]); }
       }
@@ -1641,6 +1697,7 @@ bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   world_bounds(hs, lo, hi);
   std::vector<TriRec64> recs;
   face_records(hs, recs);
+  bound_records(hs, recs);
   std::vector<Node64> tmp;
   std::vector<TriRec64> tris;
   if (gpu_build_lbvh(device, recs, lo, hi, std::max(1, std::min(leaf_size, kMaxLeaf)), bvh_pad(lo, hi), tmp, tris,
@@ -1654,6 +1711,7 @@ bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   hs.depth = trial.depth;
   hs.leaves = trial.leaves;
   hs.tris = std::move(tris);
+  world_records(hs);
   return true;
 }
 
@@ -1670,12 +1728,18 @@ bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   world_bounds(hs, lo, hi);
   std::vector<TriRec64> recs;
   face_records(hs, recs);
+  bound_records(hs, recs);
   std::vector<int32_t> child;
   std::vector<float> box;
   std::vector<uint8_t> leaf;
   int iters = 0;
   const int lb = std::max(1, std::min(leaf_size, kMaxLeaf));
-  if (gpu_build_ploc(device, recs, lo, hi, lb, kPlocRadius, kPlocTrav, child, box, leaf, gpu_ms, &iters) != RT_OK)
+  int radius = kPlocRadius, rule = 0;
+  float trav = kPlocTrav;
+  if (const char* e = debug_env("RT_PLOC_RADIUS")) radius = std::max(1, std::min(32, atoi(e)));
+  if (const char* e = debug_env("RT_PLOC_TRAV")) trav = std::max(0.05f, (float)atof(e));
+  if (const char* e = debug_env("RT_PLOC_RULE")) rule = atoi(e);
+  if (gpu_build_ploc(device, recs, lo, hi, lb, radius, trav, child, box, leaf, gpu_ms, &iters, rule) != RT_OK)
     return false;
   const int n = hs.nf, ni = n - 1, root = n - 2;
   const float pad = bvh_pad(lo, hi);
@@ -1743,6 +1807,7 @@ bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   hs.depth = trial.depth;
   hs.leaves = trial.leaves;
   hs.tris = std::move(tris);
+  world_records(hs);
   return true;
 }
 
@@ -2004,6 +2069,7 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     hs.fnn[f] = rt::normalized(f3{n[0], n[1], n[2]});
     hs.fdist[f] = rt::dot(hs.fnn[f], hs.wv[hs.fidx[3 * f]]);
   }
+  rt::accept_region(hs);
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   s->prep_ms = ms_since(t0);
@@ -2186,11 +2252,14 @@ struct Validator {
   // together cover every face
   bool strict = true;
   std::vector<std::vector<VBox>> regions;  // per face: the path-intersected boxes of its leaves (split trees)
-  static VBox tri_box(const rt::TriRec64& t) {
+  // the box of the triangle the culling must bound (rt::bound_vert: the accept region)
+  VBox tri_box(const rt::TriRec64& t) const {
     VBox b;
-    const float v[9] = {t.w0x, t.w0y, t.w0z, t.w1x, t.w1y, t.w1z, t.w2x, t.w2y, t.w2z};
-    for (int j = 0; j < 3; j++)
-      for (int k = 0; k < 3; k++) { b.lo[k] = std::min(b.lo[k], (double)v[3 * j + k]); b.hi[k] = std::max(b.hi[k], (double)v[3 * j + k]); }
+    for (int j = 0; j < 3; j++) {
+      const rt::f3& w = rt::bound_vert(hs, t.face, j);
+      const double v[3] = {w.x, w.y, w.z};
+      for (int k = 0; k < 3; k++) { b.lo[k] = std::min(b.lo[k], v[k]); b.hi[k] = std::max(b.hi[k], v[k]); }
+    }
     return b;
   }
   VBox leaf(uint32_t h, std::vector<int>& seen, const VBox& region, bool record) {
@@ -2286,9 +2355,9 @@ struct Validator {
     for (uint32_t f = 0; f < (uint32_t)hs.nf; f++) {
       const std::vector<VBox>& rs = regions[f];
       if (rs.empty()) { bad++; continue; }
-      const rt::f3& a = hs.wv[hs.fidx[3 * f]];
-      const rt::f3& b = hs.wv[hs.fidx[3 * f + 1]];
-      const rt::f3& c = hs.wv[hs.fidx[3 * f + 2]];
+      const rt::f3& a = rt::bound_vert(hs, f, 0);
+      const rt::f3& b = rt::bound_vert(hs, f, 1);
+      const rt::f3& c = rt::bound_vert(hs, f, 2);
       for (int i = 0; i <= G; i++)
         for (int j = 0; i + j <= G; j++) {
           const double s = (double)i / G, t = (double)j / G, r = 1.0 - s - t;

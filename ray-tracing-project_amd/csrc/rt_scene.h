@@ -41,6 +41,11 @@ struct HostScene {
   std::vector<f3> vnn;       // normalised vertex normals
   std::vector<f3> fnn;       // normalised face normals
   std::vector<float> fdist;  // facenormal.dot(vert0)
+  // Accept-region vertices [nf][3]: where a face normal is tilted against its world triangle (a rotating
+  // or non-uniformly scaling model matrix: the reference keeps object-space normals), the hit points the
+  // edge tests accept lie on the triangle projected along that normal onto its plane, not on the world
+  // triangle; the builders bound those (accept_region). Empty when every face is untilted.
+  std::vector<f3> av;
   std::vector<uint32_t> fidx;
   std::vector<int32_t> fmat;
   std::vector<rt_material> mats;
@@ -69,18 +74,24 @@ bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms);
 bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms);
 int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, int radius, float k_trav, std::vector<int32_t>& child2, std::vector<float>& box6,
-                   std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations);
+                   std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations, int rule);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
 void build_bvh4(HostScene& hs);
 void build_wide(HostScene& hs);
 float bvh_pad(const float lo[3], const float hi[3]);
+// fills hs.av (see HostScene::av) from wv / fnn / fdist; leaves it empty when no face needs it
+void accept_region(HostScene& hs);
+// vertex j of the triangle the culling boxes must bound for face f
+inline const f3& bound_vert(const HostScene& hs, uint32_t f, int j) {
+  return hs.av.empty() ? hs.wv[hs.fidx[3 * (size_t)f + j]] : hs.av[3 * (size_t)f + j];
+}
 float scene_static_pad(const HostScene& hs);
 float cert_origin_max(const HostScene& hs);
 uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro);  // kSafeNormalBit | kBoxCertBit of face f
 void set_error(const char* fmt, ...);
 // Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_LDS_PAD, RT_SAH_TRAV,
-// RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_TIMING): getenv(name) once rt_debug_env_knobs(1) has been called,
+// RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING): getenv(name) once rt_debug_env_knobs(1) has been called,
 // else nullptr -- the product library's behaviour never depends on the caller's environment otherwise.
 const char* debug_env(const char* name);
 void set_debug_env(bool on);

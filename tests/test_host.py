@@ -428,6 +428,54 @@ def test_box_certificates_need_a_similarity_and_matching_normals(rt, orc):
             assert cert2 == 0, (name, cert2)
 
 
+@pytest.mark.parametrize("model", ["rotated", "stretched"])
+def test_tilted_normals_trees_bound_the_accept_region(rt, orc, model):
+    """Under a rotating or non-uniformly scaling model matrix the reference tests world edges against the
+    object-space face normal n (flyscene.cpp:444-478, 573-590), so the hit points it accepts lie on the world
+    triangle projected along n onto n's plane (rt_host.cpp accept_region), up to a few % of a triangle's
+    size away from the world triangle. The oracle's hits must lie in that projection's box (the theory), a
+    good share of them outside the world triangle's box (why the builders must bound the projection), and
+    every tree must hold the projections (the validator, which checks bound_vert boxes)."""
+    path = scene_path("bunny.obj")
+    M = _rotation(20, 30) if model == "rotated" else np.diag([1.0, 0.8, 1.5, 1.0]).astype(np.float32).reshape(16)
+    om = orc.Mesh.load_obj(path)
+    om.set_model(M)
+    ex = om.export()
+    osc = orc.Scene(om)
+    for builder in (rt.RT_BUILDER_SBVH, rt.RT_BUILDER_SAH):
+        sc = rt.Scene(rt.Mesh.load_obj(path), device=rt.RT_DEVICE_NONE, shape_model_matrix=ex["M16"], builder=builder)
+        v = sc.validate_bvh()
+        assert v["ok"] and v["violations"] == 0, (builder, v)
+    Mm = np.asarray(ex["M16"], np.float64).reshape(4, 4).T
+    v4 = np.asarray(ex["v4"], np.float64)
+    wv = (Mm[:3, :3] @ (v4[:, :3] / v4[:, 3:4]).T).T + Mm[:3, 3]
+    fidx = np.asarray(ex["fidx"], np.int64)
+    n = np.asarray(ex["fn3"], np.float64)
+    n /= np.linalg.norm(n, axis=1, keepdims=True)
+    w = wv[fidx]  # [nf, 3, 3]
+    s = (np.einsum("fkc,fc->fk", w, n) - np.einsum("fc,fc->f", w[:, 0], n)[:, None])
+    proj = w - s[..., None] * n[:, None, :]
+    rng = np.random.default_rng(5)
+    lo, hi = wv.min(0), wv.max(0)
+    eye = np.array([0.4, 0.3, 2.2])
+    tgt = lo + rng.random((3000, 3)) * (hi - lo)
+    d = tgt - eye
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = np.broadcast_to(eye, d.shape).astype(np.float32)
+    face, t, P = osc.closest(o, d.astype(np.float32))
+    hit = face >= 0
+    assert hit.sum() > 500
+    f = face[hit]
+    P = np.asarray(P, np.float64)[hit]
+    diam = np.linalg.norm(w[f] - np.roll(w[f], 1, axis=1), axis=2).max(1)
+    tol = 1e-4 * diam[:, None] + 1e-6
+    pb_lo, pb_hi = proj[f].min(1), proj[f].max(1)
+    assert ((P >= pb_lo - tol) & (P <= pb_hi + tol)).all()
+    wb_lo, wb_hi = w[f].min(1), w[f].max(1)
+    outside_world = ~((P >= wb_lo - tol) & (P <= wb_hi + tol)).all(1)
+    assert outside_world.sum() > 0.01 * len(f), int(outside_world.sum())
+
+
 def test_ppm_rgb8_writer_matches_float_writer(rt, tmp_path):
     """f3: the 8-bit P3 writer produces writePPMImage's exact bytes for in-range values."""
     rng = np.random.default_rng(3)

@@ -22,6 +22,15 @@ for s in $STEPS; do
     ploc)
       timeout -k 10 300 python bench.py --steps 20 --warmup 5 --builder ploc --no-cpu --no-side > $OUT/bench_ploc.json 2> $OUT/bench_ploc.err
       rc=$?; echo "ploc rc=$rc"; cat $OUT/bench_ploc.json; hard $rc ;;
+    plocsweep)
+      # PLOC A/B: neighbour radius x collapse node cost x leaf rule (C3, --builder ploc), then the SBVH line
+      export RTAMD_DEBUG_KNOBS=1
+      for cfg in 24:0.7:0 32:0.7:0 16:0.7:0 24:0.5:0 24:1.0:0 24:0.7:1 32:0.5:1 24:1.0:1; do
+        IFS=: read r tr ru <<< "$cfg"
+        RT_PLOC_RADIUS=$r RT_PLOC_TRAV=$tr RT_PLOC_RULE=$ru timeout -k 10 120 python bench.py --steps 20 --warmup 5 \
+            --builder ploc --no-cpu --no-side --no-extra > $OUT/ploc_$cfg.json 2> $OUT/ploc_$cfg.err
+        rc=$?; echo "ploc $cfg rc=$rc $(python3 tools/ploc_line.py $OUT/ploc_$cfg.json)"; hard $rc
+      done ;;
     prof)
       OUTDIR=$OUT/prof bash tools/profile.sh > $OUT/profile.log 2>&1
       rc=$?; echo "profile rc=$rc"; tail -12 $OUT/profile.log; hard $rc ;;
