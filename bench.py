@@ -626,6 +626,7 @@ def main():
                        "kernel_ms_one_frame_alone": round(iso_ms_max, 4),
                        "host_enqueue_ms_per_frame": round(st.get("enqueue_ms", 0.0), 4),
                        "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
+                       "bvh_sah_cost": {k: round(v, 3) for k, v in sc.tree_cost().items()},
                        "wide_tree": {"nodes_per_copy": info["wide_nodes"], "depth": info["wide_depth"]} if info["wide_nodes"] else None,
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
                        "scene_setup_s_per_rank": [round(x, 2) for x in setup_per_rank],

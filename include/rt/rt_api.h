@@ -373,6 +373,11 @@ int rt_debug_math_device(int32_t op, int32_t n, const float* in, float* out);
  * each. info[0..6] = binary nodes, binary depth, quantised nodes, quantised depth, triangles reached
  * (binary), triangles reached (quantised), violations (all three trees). RT_OK iff sound. */
 int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]);
+/* Surface-area cost of the binary tree (host data, tests and A/B only): out[0] = k_trav * (interior
+ * node area sum) + (triangle-weighted leaf area sum), over the root's area -- the SAH estimate of the
+ * node steps and triangle tests of a random ray; out[1] = its node term, out[2] = its triangle term,
+ * out[3] = the mean leaf size. */
+int rt_debug_tree_cost(const rt_scene* s, double k_trav, double out[4]);
 /* Record layout of the device node allocation for a scene of n_nodes binary nodes, n_tris triangle
  * records and n_wide fp32 4-wide nodes per octant copy (host only, no device): out[0] = allocation bytes
  * (0: records exceed 4 GiB), out[1] = byte offset of the wide copies (0: the wide tree is dropped because

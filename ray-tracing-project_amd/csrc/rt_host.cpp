@@ -2397,6 +2397,51 @@ extern "C" int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float*
   return RT_OK;
 }
 
+extern "C" int rt_debug_tree_cost(const rt_scene* s, double k_trav, double out[4]) {
+  if (!s || !out) { rt::set_error("rt_debug_tree_cost: null argument"); return RT_ERR_INVALID; }
+  const rt::HostScene& hs = s->hs;
+  for (int k = 0; k < 4; k++) out[k] = 0.0;
+  if (hs.nodes.empty()) return RT_OK;
+  auto area = [](const float* b) {  // lx hx ly hy lz hz
+    const double dx = (double)b[1] - b[0], dy = (double)b[3] - b[2], dz = (double)b[5] - b[4];
+    return dx < 0 || dy < 0 || dz < 0 ? 0.0 : dx * dy + dy * dz + dz * dx;
+  };
+  double inner = 0.0, leafc = 0.0, leaves = 0.0, tris = 0.0;
+  std::vector<std::pair<uint32_t, double>> st{{hs.root, -1.0}};
+  double root_area = 0.0;
+  while (!st.empty()) {
+    const auto [h, a] = st.back();
+    st.pop_back();
+    if (rt::is_leaf(h)) {
+      leafc += a * rt::leaf_count(h);
+      leaves += 1;
+      tris += rt::leaf_count(h);
+      continue;
+    }
+    const rt::Node64& nd = hs.nodes[h];
+    const float* b0 = &nd.c0lx;
+    const float* b1 = &nd.c1lx;
+    double an = a;
+    if (an < 0) {  // the root: the union of its children's boxes
+      float u[6];
+      for (int k = 0; k < 3; k++) {
+        u[2 * k] = std::min(b0[2 * k], b1[2 * k]);
+        u[2 * k + 1] = std::max(b0[2 * k + 1], b1[2 * k + 1]);
+      }
+      an = root_area = area(u);
+    }
+    inner += an;
+    st.push_back({nd.child0, area(b0)});
+    st.push_back({nd.child1, area(b1)});
+  }
+  if (!(root_area > 0)) return RT_OK;
+  out[0] = (k_trav * inner + leafc) / root_area;  // SAH cost in triangle tests per random ray
+  out[1] = inner / root_area;                      // expected node visits (interior) per random ray
+  out[2] = leafc / root_area;                      // expected triangle tests per random ray
+  out[3] = leaves > 0 ? tris / leaves : 0.0;       // mean leaf size
+  return RT_OK;
+}
+
 extern "C" int rt_debug_validate_bvh(const rt_scene* s, int64_t info[7]) {
   if (!s || !info) { rt::set_error("rt_debug_validate_bvh: null argument"); return RT_ERR_INVALID; }
   const rt::HostScene& hs = s->hs;

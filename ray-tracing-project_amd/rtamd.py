@@ -32,7 +32,7 @@ EXPORTS = [
     "rt_frame_unpack_shards_rgb8", "rt_rand_seed", "rt_rand", "rt_lights_spherical", "rt_light_directional",
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
     "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
-    "rt_debug_record_layout", "rt_debug_scene_flags", "rt_debug_env_knobs",
+    "rt_debug_record_layout", "rt_debug_scene_flags", "rt_debug_env_knobs", "rt_debug_tree_cost",
 ]
 
 
@@ -140,6 +140,7 @@ def lib():
         L.rt_debug_validate_bvh.argtypes = [vp, vp]
         L.rt_debug_record_layout.argtypes = [C.c_int64, C.c_int64, C.c_int64, vp]
         L.rt_debug_scene_flags.argtypes = [vp, vp, vp, vp]
+        L.rt_debug_tree_cost.argtypes = [vp, C.c_double, vp]
         L.rt_debug_set_variant.argtypes = [C.c_int32]
         L.rt_debug_env_knobs.argtypes = [C.c_int32]
         # A/B and diagnostic environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SAH_TRAV, RT_TIMING, ...):
@@ -331,6 +332,12 @@ class Scene:
         t = np.zeros((H, W), np.float32) if want_hits else None
         check(lib().rt_frame_download(self.h, W * H, _p(rgb), _p(face), _p(t)))
         return (rgb, face, t) if want_hits else rgb
+
+    def tree_cost(self, k_trav=0.7):
+        """rt_debug_tree_cost: SAH cost, node term, triangle term, mean leaf size of the binary tree."""
+        out = np.zeros(4, np.float64)
+        check(lib().rt_debug_tree_cost(self.h, float(k_trav), _p(out)))
+        return dict(sah=float(out[0]), nodes=float(out[1]), tris=float(out[2]), leaf=float(out[3]))
 
     def record_flags(self):
         """rt_debug_scene_flags: (triangle records, with the safe-normal bit, with the box certificate)."""

@@ -31,6 +31,15 @@ for s in $STEPS; do
             --builder ploc --no-cpu --no-side --no-extra > $OUT/ploc_$cfg.json 2> $OUT/ploc_$cfg.err
         rc=$?; echo "ploc $cfg rc=$rc $(python3 tools/ploc_line.py $OUT/ploc_$cfg.json)"; hard $rc
       done ;;
+    builders)
+      # the same C3 line per builder (SBVH default, host binned SAH, device LBVH) and PLOC radii
+      export RTAMD_DEBUG_KNOBS=1
+      for cfg in ${BUILDERS:-sbvh sah lbvh ploc:4 ploc:8 ploc:12 ploc:16}; do
+        IFS=: read b r <<< "$cfg"
+        RT_PLOC_RADIUS=${r:-24} timeout -k 10 120 python bench.py --steps 20 --warmup 5 --builder $b --no-cpu --no-side \
+            --no-extra > $OUT/builder_$cfg.json 2> $OUT/builder_$cfg.err
+        rc=$?; echo "builder $cfg rc=$rc $(python3 tools/ploc_line.py $OUT/builder_$cfg.json)"; hard $rc
+      done ;;
     prof)
       OUTDIR=$OUT/prof bash tools/profile.sh > $OUT/profile.log 2>&1
       rc=$?; echo "profile rc=$rc"; tail -12 $OUT/profile.log; hard $rc ;;
