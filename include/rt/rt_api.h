@@ -112,7 +112,9 @@ typedef struct rt_scene_opts {
                              * (Morton/radix-sort/Karras build on the device in milliseconds;
                              * falls back to RT_BUILDER_SAH when the tree would be too deep) or
                              * RT_BUILDER_PLOC_GPU (parallel locally-ordered clustering on the
-                             * device, SAH-quality tree in milliseconds; same fallback) */
+                             * device in milliseconds; same fallback) or RT_BUILDER_SAH_GPU (the host
+                             * binned-SAH algorithm run top-down on the device, one level per round of
+                             * launches; same fallback) */
   int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_HOST (default,
                              * parallel passes on the host) or RT_BOXES_GPU (one launch per pass,
                              * one workgroup per box; identical boxes and face order; scenes with
@@ -128,6 +130,7 @@ typedef struct rt_scene_opts {
 #define RT_BUILDER_LBVH_GPU 1
 #define RT_BUILDER_SBVH 2
 #define RT_BUILDER_PLOC_GPU 3
+#define RT_BUILDER_SAH_GPU 4
 #define RT_BOXES_HOST 0
 #define RT_BOXES_GPU 1
 

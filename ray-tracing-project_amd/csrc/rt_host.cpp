@@ -1811,6 +1811,54 @@ bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   return true;
 }
 
+// GPU top-down binned SAH (rt_build.hip gpu_build_sah) + host layout: interior node 0 is the root, child
+// handles are node ids or leaf handles over the returned slot order; the host pads the boxes and re-lays
+// the nodes out depth first. false (nothing changed) when the device build is impossible or too deep.
+bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
+  if (hs.nf < 2) return false;
+  float lo[3], hi[3];
+  world_bounds(hs, lo, hi);
+  std::vector<TriRec64> recs;
+  face_records(hs, recs);
+  bound_records(hs, recs);
+  std::vector<uint32_t> nchild, slot_face;
+  std::vector<float> ncb;
+  int levels = 0;
+  float trav = 0.7f;
+  if (const char* e = debug_env("RT_SAH_TRAV")) trav = std::max(0.05f, (float)atof(e));
+  if (gpu_build_sah(device, recs, lo, hi, std::max(1, std::min(leaf_size, kMaxLeaf)), trav, nchild, ncb, slot_face, gpu_ms,
+                    &levels) != RT_OK)
+    return false;
+  const size_t nn = nchild.size() / 2;
+  const float pad = bvh_pad(lo, hi);
+  std::vector<Node64> tmp(nn);
+  for (size_t k = 0; k < nn; k++) {
+    Node64 nd{};
+    for (int side = 0; side < 2; side++) {
+      const float* b = &ncb[12 * k + 6 * side];  // lo xyz, hi xyz
+      const uint32_t h = nchild[2 * k + side];
+      if (!is_leaf(h) && h >= nn) return false;
+      float* o = side ? &nd.c1lx : &nd.c0lx;  // lx hx ly hy lz hz
+      o[0] = b[0] - pad; o[1] = b[3] + pad; o[2] = b[1] - pad; o[3] = b[4] + pad; o[4] = b[2] - pad; o[5] = b[5] + pad;
+      (side ? nd.child1 : nd.child0) = h;
+    }
+    tmp[k] = nd;
+  }
+  HostScene trial;
+  relayout_dfs(trial, tmp, 0);
+  if (trial.depth > kMaxDepth + 2) return false;  // too deep for the wave stack: host SAH instead
+  if (debug_env("RT_TIMING")) fprintf(stderr, "[rt] sah-gpu: %d levels, %zu nodes, depth %d\n", levels, nn, trial.depth);
+  std::vector<TriRec64> tris(slot_face.size());
+  for (size_t sl = 0; sl < slot_face.size(); sl++) tris[sl] = recs[slot_face[sl]];
+  hs.nodes = std::move(trial.nodes);
+  hs.root = 0;
+  hs.depth = trial.depth;
+  hs.leaves = trial.leaves;
+  hs.tris = std::move(tris);
+  world_records(hs);
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // 4-wide collapse: each wide node takes a binary node's two children and keeps opening the interior
 // child with the largest surface area until it has four children (or only leaves remain). Child
@@ -2097,6 +2145,12 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
             s->box_builder_used == RT_BOXES_GPU ? "gpu" : "host", s->boxes_gpu_ms, hs.boxes.size());
   auto t2 = clk::now();
   bool built = false;
+  if (s->opts.builder == RT_BUILDER_SAH_GPU && s->opts.device != RT_DEVICE_NONE) {
+    int dev = s->opts.device;
+    if (dev < 0) dev = rt::current_device();
+    built = dev >= 0 && rt::build_bvh_sah_gpu(hs, dev, leaf, &s->bvh_gpu_ms);
+    if (built) s->builder_used = RT_BUILDER_SAH_GPU;
+  }
   if (s->opts.builder == RT_BUILDER_PLOC_GPU && s->opts.device != RT_DEVICE_NONE) {
     int dev = s->opts.device;
     if (dev < 0) dev = rt::current_device();

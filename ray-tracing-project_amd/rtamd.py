@@ -285,7 +285,7 @@ class Mesh:
             self.h = None
 
 
-RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH, RT_BUILDER_PLOC_GPU = 0, 1, 2, 3
+RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH, RT_BUILDER_PLOC_GPU, RT_BUILDER_SAH_GPU = 0, 1, 2, 3, 4
 RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 

@@ -220,14 +220,15 @@ def test_gpu_lbvh_soup_matches_oracle_digests(rt, scenes):
     assert sha(face) == DIG["C3"]["face_sha256"] and sha(t) == DIG["C3"]["t_sha256"]
 
 
-@pytest.mark.parametrize("case", ["C2", "C3", "C5"])
-def test_gpu_ploc_frames_match_oracle_digests(rt, scenes, case):
-    """f2 PLOC on the BASELINE configs: the device-built tree's full 1080p frames (C2 bunny PRIMARY, C3 soup
-    PRIMARY, C5 bunny FULL) have the oracle's face / t digests."""
+@pytest.mark.parametrize("case,builder", [("C2", "ploc"), ("C3", "ploc"), ("C5", "ploc"), ("C3", "sahgpu"), ("C5", "sahgpu")])
+def test_gpu_ploc_frames_match_oracle_digests(rt, scenes, case, builder):
+    """f2 PLOC and the device binned SAH on the BASELINE configs: the device-built tree's full 1080p frames
+    (C2 bunny PRIMARY, C3 soup PRIMARY, C5 bunny FULL) have the oracle's face / t digests."""
     d = DIG[case]
     mesh = scenes["bunny_mesh"] if d["scene"] == "bunny" else scenes["soup_mesh"]
-    pl = rt.Scene(mesh, builder=rt.RT_BUILDER_PLOC_GPU)
-    assert pl.info()["builder"] == rt.RT_BUILDER_PLOC_GPU
+    bid = rt.RT_BUILDER_PLOC_GPU if builder == "ploc" else rt.RT_BUILDER_SAH_GPU
+    pl = rt.Scene(mesh, builder=bid)
+    assert pl.info()["builder"] == bid
     rgb, face, t = gpu_frame(rt, pl, d["W"], d["H"], d["mode"])
     assert sha(face) == d["face_sha256"] and sha(t) == d["t_sha256"], case
 

@@ -401,12 +401,18 @@ def test_gpu_lbvh_builder(rt, soup, name):
             assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (name, m)
 
 
-@pytest.mark.parametrize("name", ["bunny", "soup"])
-def test_gpu_ploc_builder(rt, soup, name):
-    """f2 "LBVH/PLOC": the device PLOC build (rt_build.hip) gives a sound tree -- every triangle inside every
+@pytest.mark.parametrize("builder", ["ploc", "sahgpu"])
+@pytest.mark.parametrize("name", ["bunny", "soup", "cube"])
+def test_gpu_ploc_builder(rt, soup, name, builder):
+    """f2 "LBVH/PLOC" and the device binned SAH (rt_build.hip) give a sound tree -- every triangle inside every
     ancestor box, every face in exactly one leaf, leaves of at most 4 triangles -- and the frame of the
-    host-SBVH scene bit for bit (PRIMARY and FULL)."""
-    if name == "bunny":
+    host-SBVH scene bit for bit (PRIMARY and FULL); the 12-triangle cube takes the small-task paths only."""
+    bid = rt.RT_BUILDER_PLOC_GPU if builder == "ploc" else rt.RT_BUILDER_SAH_GPU
+    if name == "cube":
+        mesh = rt.Mesh.load_obj(scene_path("cube.obj"))
+        ref = rt.Scene(mesh)
+        W, H = 320, 240
+    elif name == "bunny":
         mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
         ref = rt.Scene(mesh)
         W, H = 1920, 1080
@@ -414,9 +420,9 @@ def test_gpu_ploc_builder(rt, soup, name):
         ref, _ = soup
         mesh = ref.mesh
         W, H = 960, 540
-    pl = rt.Scene(mesh, builder=rt.RT_BUILDER_PLOC_GPU)
+    pl = rt.Scene(mesh, builder=bid)
     info = pl.info()
-    assert info["builder"] == rt.RT_BUILDER_PLOC_GPU and info["bvh_gpu_ms"] > 0
+    assert info["builder"] == bid and info["bvh_gpu_ms"] > 0
     assert info["bvh_depth"] <= 62
     v = pl.validate_bvh()
     assert v["ok"] and v["covered2"] == info["n_faces"], v
