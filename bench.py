@@ -439,9 +439,9 @@ def main():
     ap.add_argument("--no-shared-build", action="store_true",
                     help="N > 1: every rank builds the scene itself instead of loading rank 0's scene cache")
     ap.add_argument("--leaf", type=int, default=0, help="BVH leaf size bound (0 = library default)")
-    ap.add_argument("--builder", choices=["sbvh", "sah", "lbvh", "ploc", "sahgpu"], default="sbvh",
-                    help="BVH builder: host SAH with spatial splits (default), host binned SAH, or the device LBVH "
-                         "or PLOC (SURVEY f2)")
+    ap.add_argument("--builder", choices=["sbvh", "sah", "lbvh", "ploc", "sahgpu", "sbvhgpu"], default="sbvhgpu",
+                    help="BVH builder: SAH with spatial splits on the device (default) or the host, binned SAH on "
+                         "the host or the device, or the device LBVH or PLOC (SURVEY f2)")
     ap.add_argument("--wide", action="store_true",
                     help="also build the fp32 4-wide tree and walk it for PRIMARY packets (rt_scene_opts.wide_tree)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
@@ -496,7 +496,8 @@ def main():
     else:
         scene_name = "Stanford bunny (69,451 triangles)"
     builder = {"lbvh": rt.RT_BUILDER_LBVH_GPU, "sah": rt.RT_BUILDER_SAH, "sbvh": rt.RT_BUILDER_SBVH,
-               "ploc": rt.RT_BUILDER_PLOC_GPU, "sahgpu": rt.RT_BUILDER_SAH_GPU}[a.builder]
+               "ploc": rt.RT_BUILDER_PLOC_GPU, "sahgpu": rt.RT_BUILDER_SAH_GPU,
+               "sbvhgpu": rt.RT_BUILDER_SBVH_GPU}[a.builder]
 
     def build_scene():
         if a.scene == "soup":
@@ -631,7 +632,7 @@ def main():
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
                        "scene_setup_s_per_rank": [round(x, 2) for x in setup_per_rank],
                        "scene_shared_build": cache_path is not None,
-                       "builder": {0: "sah-host", 1: "lbvh-gpu", 2: "sbvh-host", 3: "ploc-gpu", 4: "sah-gpu"}.get(info["builder"], str(info["builder"])),
+                       "builder": {0: "sah-host", 1: "lbvh-gpu", 2: "sbvh-host", 3: "ploc-gpu", 4: "sah-gpu", 5: "sbvh-gpu"}.get(info["builder"], str(info["builder"])),
                        "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
                                     "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),
                                     "upload": round(info["upload_ms"], 1)}, **more},

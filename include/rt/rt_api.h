@@ -106,15 +106,18 @@ typedef struct rt_scene_opts {
                              * costs (small scenes also split their costliest waves); results never
                              * depend on the dispatch order */
   int32_t builder;          /* the traversal tree's builder (results never depend on it):
-                             * RT_BUILDER_SBVH (rt_scene_opts_default: host SAH with spatial splits, the
-                             * fastest traversal; 1M faces ~4-5 s), RT_BUILDER_SAH (host binned SAH without
+                             * RT_BUILDER_SBVH_GPU (rt_scene_opts_default: SAH with spatial splits built on
+                             * the device, 1M faces ~0.1 s of kernels; host RT_BUILDER_SBVH without a device or
+                             * when the tree would be too deep), RT_BUILDER_SBVH (the same tree quality on the
+                             * host; 1M faces 2-5 s), RT_BUILDER_SAH (host binned SAH without
                              * splits: ~4x faster build, ~5% slower traversal) or RT_BUILDER_LBVH_GPU
                              * (Morton/radix-sort/Karras build on the device in milliseconds;
                              * falls back to RT_BUILDER_SAH when the tree would be too deep) or
                              * RT_BUILDER_PLOC_GPU (parallel locally-ordered clustering on the
                              * device in milliseconds; same fallback) or RT_BUILDER_SAH_GPU (the host
                              * binned-SAH algorithm run top-down on the device, one level per round of
-                             * launches; same fallback) */
+                             * launches; same fallback) or RT_BUILDER_SBVH_GPU (the same with the host
+                             * SBVH's spatial splits; same fallback) */
   int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_HOST (default,
                              * parallel passes on the host) or RT_BOXES_GPU (one launch per pass,
                              * one workgroup per box; identical boxes and face order; scenes with
@@ -131,6 +134,7 @@ typedef struct rt_scene_opts {
 #define RT_BUILDER_SBVH 2
 #define RT_BUILDER_PLOC_GPU 3
 #define RT_BUILDER_SAH_GPU 4
+#define RT_BUILDER_SBVH_GPU 5
 #define RT_BOXES_HOST 0
 #define RT_BOXES_GPU 1
 

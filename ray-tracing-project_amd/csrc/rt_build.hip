@@ -488,28 +488,44 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
 
 
 // ---------------------------------------------------------------------------------------------------
-// Top-down binned SAH on the GPU (RT_BUILDER_SAH_GPU): the host SAH builder's algorithm -- 32 centroid
-// bins per axis, cost k_trav * A + sum(n_side * A_side), leaf when <= leaf_size triangles and no costlier
-// -- run breadth first, one level of the tree per round of launches. Triangles keep their Morton order
-// inside every node's contiguous range (stable partition by one scan), so small tasks stay coherent.
-//   per level: (1) every active task's box and centroid bounds: a segmented wave reduction over its
-//   contiguous positions, one atomic per segment and wave; (2) tasks above kSahSmall triangles: centroid
-//   bins (ordered-uint atomics; a block whose 256 positions belong to one task bins in LDS first);
-//   (3) one thread per task picks the split: the bins' sweep for big tasks, an exact sweep over the sorted
-//   centroids (<= kSahSmall) for small ones, the object median when the centroids are degenerate or the
-//   depth is near the stack bound; a leaf writes its handle into its parent, a split allocates its node
-//   and two child tasks; (4) the side of every position; (5) one exclusive scan and a scatter.
+// Top-down binned SAH on the GPU, with or without spatial splits (RT_BUILDER_SAH_GPU / RT_BUILDER_SBVH_GPU):
+// the host builders' algorithms (32 centroid bins per axis, cost k_trav * A + sum(n_side * A_side), a leaf
+// when <= leaf_size references and no costlier; SBVH: 32 spatial bins per axis tried when the object
+// split's children overlap by more than alpha of the root, straddling triangles clipped to both sides,
+// duplication bounded by a per-subtree budget divided in proportion to the children) run breadth first,
+// one level of the tree per round of launches. References keep their Morton order inside every node's
+// contiguous range (stable partition), so small tasks stay coherent. Per level:
+//   (1) every active task's box and centroid bounds: a segmented wave reduction over its contiguous
+//       positions, one atomic per segment and wave;
+//   (2) tasks above kSahSmall references: centroid bins (ordered-uint atomics; a block whose 256 positions
+//       belong to one task bins in LDS first); one thread per task sweeps them (phase A) and flags the
+//       tasks whose object split overlaps enough for a spatial split, which then bin their references'
+//       clipped parts (SBVH only);
+//   (3) one thread per task decides: the cheaper of the object and spatial split for big tasks, an exact
+//       sweep over the sorted centroids (<= kSahSmall) for small ones, the position median when the
+//       centroids are degenerate or the depth nears the stack bound; a leaf takes a leaf id, a split its
+//       node and two child tasks;
+//   (4) every position's sides (left, right or both for a clipped straddler) and two exclusive scans give
+//       every output position; the child tasks get their ranges; (5) one scatter writes the next level.
+// Leaves are resolved to slot ranges at the end (their references move while others duplicate).
 // ---------------------------------------------------------------------------------------------------
 namespace {
 constexpr int kSahBins = 32, kSahSmall = 16, kSahBlock = 256;
+constexpr int kObjW = 7, kSpW = 8;  // words per object bin (box lo, hi as ordered uints; count) / spatial bin (+ exits)
 
 struct SahTask {
-  uint32_t begin, count;
-  int32_t parent_slot;  // 2 * parent node + side, -1 for the root
-  int32_t big;          // bin block index (count > kSahSmall) or -1
-  int32_t child;        // first child task of the next level, -1 for a leaf
-  int32_t axis, bin;    // split: axis and last left bin (bin -1: position median / exact sweep sides)
-  uint32_t nleft;
+  uint32_t begin, count;  // reference range at this level
+  int32_t parent_slot;    // 2 * parent node + side, -1 for the root
+  int32_t big;            // object-bin block (count > kSahSmall) or -1
+  int32_t sp;             // spatial-bin block or -1
+  int32_t child;          // first child task of the next level; -1: a leaf (bin = its leaf id)
+  int32_t axis, bin;      // >= 0: object split (last left bin); -1: position median (bin = left count);
+                          // -2: sides from the exact sweep; 3..5: spatial split on axis - 3 at `plane`
+  float plane;
+  int32_t budget;         // references this subtree may add by spatial splits
+  float o_cost;           // phase A: the best object split
+  int32_t o_axis, o_bin;
+  uint32_t o_nl;
 };
 
 __device__ __forceinline__ uint32_t f2o(float f) {
@@ -522,41 +538,83 @@ __device__ __forceinline__ float sah_area(const float* lo, const float* hi) {
   const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
   return dx * dy + dy * dz + dz * dx;
 }
-__device__ __forceinline__ int sah_bin(float c, float lo, float sc) {
-  return min(kSahBins - 1, (int)((c - lo) * sc));
+__device__ __forceinline__ int sah_bin(float c, float lo, float sc) { return min(kSahBins - 1, (int)((c - lo) * sc)); }
+__device__ __forceinline__ bool is_lo_word(int k) { return k < 3 || (k >= 6 && k < 9); }
+
+// spatial bin planes of a task box on axis k: pl(i) = lo + w * i, pl(kSahBins) = hi (as the host builder)
+__device__ __forceinline__ float sp_plane(const Box6& b, int k, int i) {
+  const float w = (b.hi[k] - b.lo[k]) / kSahBins;
+  return i >= kSahBins ? b.hi[k] : b.lo[k] + w * i;
+}
+__device__ __forceinline__ int sp_bin(const Box6& b, int k, float x) {
+  const float w = (b.hi[k] - b.lo[k]) / kSahBins;
+  int bi = min(kSahBins - 1, max(0, (int)((x - b.lo[k]) / w)));
+  while (bi > 0 && x < sp_plane(b, k, bi)) bi--;
+  while (bi < kSahBins - 1 && x >= sp_plane(b, k, bi + 1)) bi++;
+  return bi;
+}
+__device__ __forceinline__ float fdown(double x) { const float f = (float)x; return (double)f > x ? nextafterf(f, -INFINITY) : f; }
+__device__ __forceinline__ float fup(double x) { const float f = (float)x; return (double)f < x ? nextafterf(f, INFINITY) : f; }
+// bounds of triangle `t` (its record's vertices: the culling bounds) inside [a, b] on axis k, intersected
+// with `within` (the reference's box); false if empty -- the host SBVH's clip (rt_host.cpp SbvhBuilder)
+__device__ bool clip_tri(const TriRec64& t, int k, float a, float b, const Box6& within, Box6& out) {
+  const double v[3][3] = {{t.w0x, t.w0y, t.w0z}, {t.w1x, t.w1y, t.w1z}, {t.w2x, t.w2y, t.w2z}};
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int j = 0; j < 3; j++) {
+    const double* p = v[j];
+    const double* q = v[(j + 1) % 3];
+    if (p[k] >= a && p[k] <= b)
+      for (int i = 0; i < 3; i++) { lo[i] = fmin(lo[i], p[i]); hi[i] = fmax(hi[i], p[i]); }
+    const double pls[2] = {(double)a, (double)b};
+    for (int s = 0; s < 2; s++) {
+      const double pl = pls[s];
+      if ((p[k] < pl && q[k] > pl) || (p[k] > pl && q[k] < pl)) {
+        const double tt = (pl - p[k]) / (q[k] - p[k]);
+        for (int i = 0; i < 3; i++) {
+          const double x = i == k ? pl : p[i] + tt * (q[i] - p[i]);
+          lo[i] = fmin(lo[i], x);
+          hi[i] = fmax(hi[i], x);
+        }
+      }
+    }
+  }
+  for (int i = 0; i < 3; i++) {
+    out.lo[i] = fmaxf(fdown(lo[i]), within.lo[i]);
+    out.hi[i] = fminf(fup(hi[i]), within.hi[i]);
+    if (i == k) { out.lo[i] = fmaxf(out.lo[i], a); out.hi[i] = fminf(out.hi[i], b); }
+    if (!(out.lo[i] <= out.hi[i])) return false;
+  }
+  return true;
 }
 
-__global__ void k_sah_init(const uint64_t* keys, const TriRec64* rec, int n, Box6* pbox, uint32_t* idx, int32_t* ptask) {
+__global__ void k_sah_init(const uint64_t* keys, const TriRec64* rec, int n, uint32_t* rface, Box6* rbox, int32_t* ptask) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t f = (uint32_t)keys[i];
-  pbox[f] = tri_box(rec[f]);
-  idx[i] = f;
+  rface[i] = f;
+  rbox[i] = tri_box(rec[f]);
   ptask[i] = 0;
 }
-
 __global__ void k_sah_stat_init(uint32_t* stat, int ntask) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntask) return;
-  uint32_t* s = stat + 12 * (size_t)t;
-  for (int k = 0; k < 12; k++) s[k] = (k < 3 || (k >= 6 && k < 9)) ? 0xFFFFFFFFu : 0u;
+  for (int k = 0; k < 12; k++) stat[12 * (size_t)t + k] = is_lo_word(k) ? 0xFFFFFFFFu : 0u;
 }
-__global__ void k_sah_bins_init(uint32_t* bins, int nbig) {
+// bins of `w` words: the first three start at all-ones (ordered minima), the rest at 0
+__global__ void k_sah_bins_init(uint32_t* bins, int nbins, int w) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbig * 3 * kSahBins) return;
-  uint32_t* d = bins + 7 * (size_t)b;
-  for (int q = 0; q < 7; q++) d[q] = q < 3 ? 0xFFFFFFFFu : 0u;
+  if (b >= nbins) return;
+  for (int q = 0; q < w; q++) bins[(size_t)w * b + q] = q < 3 ? 0xFFFFFFFFu : 0u;
 }
 
-// (1) box and centroid bounds of every active task (stat[t]: 12 ordered uints: box lo, box hi, cen lo, cen hi)
-__global__ __launch_bounds__(kSahBlock) void k_sah_bounds(const Box6* pbox, const uint32_t* idx, const int32_t* ptask,
-                                                         int n, uint32_t* stat) {
+// (1) box and centroid bounds of every active task (stat[t]: box lo, box hi, centroid lo, centroid hi)
+__global__ __launch_bounds__(kSahBlock) void k_sah_bounds(const Box6* rbox, const int32_t* ptask, int m, uint32_t* stat) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  const int t = i < n ? ptask[i] : -1;
+  const int t = i < m ? ptask[i] : -1;
   uint32_t v[12];
   if (t >= 0) {
-    const Box6 b = pbox[idx[i]];
+    const Box6 b = rbox[i];
     for (int k = 0; k < 3; k++) {
       v[k] = f2o(b.lo[k]);
       v[3 + k] = f2o(b.hi[k]);
@@ -565,119 +623,206 @@ __global__ __launch_bounds__(kSahBlock) void k_sah_bounds(const Box6* pbox, cons
   } else {
     for (int k = 0; k < 12; k++) v[k] = 0;
   }
-  // segmented inclusive scan (min for the lo halves, max for the hi halves) over equal task ids
+  // segmented inclusive scan over equal task ids (a task's positions are contiguous)
   for (int off = 1; off < 64; off <<= 1) {
     const int tu = __shfl_up(t, off, 64);
     const bool take = lane >= off && tu == t;
     for (int k = 0; k < 12; k++) {
       const uint32_t u = __shfl_up(v[k], off, 64);
-      const bool lo = (k < 3) || (k >= 6 && k < 9);
-      if (take) v[k] = lo ? min(v[k], u) : max(v[k], u);
+      if (take) v[k] = is_lo_word(k) ? min(v[k], u) : max(v[k], u);
     }
   }
   const int tn = __shfl_down(t, 1, 64);
-  if (t >= 0 && (lane == 63 || tn != t || i == n - 1)) {
+  if (t >= 0 && (lane == 63 || tn != t || i == m - 1)) {
     uint32_t* s = stat + 12 * (size_t)t;
     for (int k = 0; k < 12; k++) {
-      const bool lo = (k < 3) || (k >= 6 && k < 9);
-      if (lo) atomicMin(&s[k], v[k]); else atomicMax(&s[k], v[k]);
+      if (is_lo_word(k)) atomicMin(&s[k], v[k]); else atomicMax(&s[k], v[k]);
     }
   }
 }
 
-// (2) centroid bins of the big tasks: bins[big][axis][bin] = 7 uints (box lo, box hi ordered; count)
-__global__ __launch_bounds__(kSahBlock) void k_sah_bin(const Box6* pbox, const uint32_t* idx, const int32_t* ptask,
-                                                      const SahTask* task, const uint32_t* stat, int n, uint32_t* bins) {
-  __shared__ uint32_t lb[3 * kSahBins * 7];
+// (2) centroid bins of the big tasks
+__global__ __launch_bounds__(kSahBlock) void k_sah_bin(const Box6* rbox, const int32_t* ptask, const SahTask* task,
+                                                      const uint32_t* stat, int m, uint32_t* bins) {
+  __shared__ uint32_t lb[3 * kSahBins * kObjW];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int first = blockIdx.x * blockDim.x, last = min(n - 1, first + kSahBlock - 1);
+  const int first = blockIdx.x * blockDim.x, last = min(m - 1, first + kSahBlock - 1);
   const int t0 = ptask[first], t1 = ptask[last];
-  const bool uniform_task = t0 == t1 && t0 >= 0 && task[t0].big >= 0;  // block-uniform
-  const int t = i < n ? ptask[i] : -1;
-  if (uniform_task) {
-    for (int k = threadIdx.x; k < 3 * kSahBins * 7; k += kSahBlock) lb[k] = (k % 7) < 3 ? 0xFFFFFFFFu : 0u;
+  const bool one_task = t0 == t1 && t0 >= 0 && task[t0].big >= 0;  // block-uniform
+  const int t = i < m ? ptask[i] : -1;
+  if (one_task) {
+    for (int k = threadIdx.x; k < 3 * kSahBins * kObjW; k += kSahBlock) lb[k] = (k % kObjW) < 3 ? 0xFFFFFFFFu : 0u;
     __syncthreads();
   }
   if (t >= 0 && task[t].big >= 0) {
     const uint32_t* s = stat + 12 * (size_t)t;
-    const Box6 b = pbox[idx[i]];
+    const Box6 b = rbox[i];
     const uint32_t bl[3] = {f2o(b.lo[0]), f2o(b.lo[1]), f2o(b.lo[2])}, bh[3] = {f2o(b.hi[0]), f2o(b.hi[1]), f2o(b.hi[2])};
-    uint32_t* gb = bins + (size_t)task[t].big * 3 * kSahBins * 7;
+    uint32_t* gb = bins + (size_t)task[t].big * 3 * kSahBins * kObjW;
     for (int k = 0; k < 3; k++) {
       const float clo = o2f(s[6 + k]), ext = o2f(s[9 + k]) - clo;
       if (!(ext > 0.0f)) continue;
       const int bi = sah_bin(cen(b, k), clo, kSahBins / ext);
-      uint32_t* d = (uniform_task ? lb : gb) + (k * kSahBins + bi) * 7;
+      uint32_t* d = (one_task ? lb : gb) + (k * kSahBins + bi) * kObjW;
       for (int q = 0; q < 3; q++) { atomicMin(&d[q], bl[q]); atomicMax(&d[3 + q], bh[q]); }
       atomicAdd(&d[6], 1u);
     }
   }
-  if (uniform_task) {
+  if (one_task) {
     __syncthreads();
-    uint32_t* gb = bins + (size_t)task[t0].big * 3 * kSahBins * 7;
+    uint32_t* gb = bins + (size_t)task[t0].big * 3 * kSahBins * kObjW;
     for (int k = threadIdx.x; k < 3 * kSahBins; k += kSahBlock) {
-      const uint32_t* d = lb + k * 7;
+      const uint32_t* d = lb + k * kObjW;
       if (d[6] == 0) continue;
-      uint32_t* g = gb + k * 7;
+      uint32_t* g = gb + k * kObjW;
       for (int q = 0; q < 3; q++) { atomicMin(&g[q], d[q]); atomicMax(&g[3 + q], d[3 + q]); }
       atomicAdd(&g[6], d[6]);
     }
   }
 }
 
-// (3) the split of every task of the level
-__global__ void k_sah_split(SahTask* task, int ntask, const uint32_t* stat, const uint32_t* bins, const Box6* pbox,
-                            const uint32_t* idx, uint8_t* side, SahTask* next, uint32_t* counters, uint32_t* nchild,
-                            Box6* ncb, int leaf_size, float k_trav, int force_median) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntask) return;
-  SahTask T = task[t];
-  const uint32_t* s = stat + 12 * (size_t)t;
-  Box6 box;
-  float clo[3], ext[3];
+__device__ __forceinline__ void task_box(const uint32_t* s, Box6& box, float* clo, float* ext) {
   for (int k = 0; k < 3; k++) {
     box.lo[k] = o2f(s[k]);
     box.hi[k] = o2f(s[3 + k]);
     clo[k] = o2f(s[6 + k]);
     ext[k] = o2f(s[9 + k]) - clo[k];
   }
+}
+
+// (2, phase A) the best object split of every big task, and whether a spatial split is to be tried
+__global__ void k_sah_split_obj(SahTask* task, int ntask, const uint32_t* stat, const uint32_t* bins, uint32_t* counters,
+                                float root_area, float alpha, int spatial, int force_median) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntask) return;
+  SahTask T = task[t];
+  T.o_cost = INFINITY;
+  T.o_axis = -1;
+  T.o_bin = -1;
+  T.o_nl = 0;
+  T.sp = -1;
+  if (T.big < 0 || force_median) { task[t] = T; return; }
+  Box6 box;
+  float clo[3], ext[3];
+  task_box(stat + 12 * (size_t)t, box, clo, ext);
+  const uint32_t* B = bins + (size_t)T.big * 3 * kSahBins * kObjW;
+  Box6 lbest, rbest;
+  for (int k = 0; k < 3; k++) {
+    if (!(ext[k] > 0.0f)) continue;
+    Box6 racc[kSahBins];
+    uint32_t rcnt[kSahBins];
+    Box6 acc{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+    uint32_t c = 0;
+    for (int i = kSahBins - 1; i > 0; i--) {
+      const uint32_t* d = B + (k * kSahBins + i) * kObjW;
+      if (d[6]) for (int q = 0; q < 3; q++) { acc.lo[q] = fminf(acc.lo[q], o2f(d[q])); acc.hi[q] = fmaxf(acc.hi[q], o2f(d[3 + q])); }
+      c += d[6];
+      racc[i] = acc;
+      rcnt[i] = c;
+    }
+    Box6 lacc{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+    uint32_t lc = 0;
+    for (int i = 0; i < kSahBins - 1; i++) {
+      const uint32_t* d = B + (k * kSahBins + i) * kObjW;
+      if (d[6]) for (int q = 0; q < 3; q++) { lacc.lo[q] = fminf(lacc.lo[q], o2f(d[q])); lacc.hi[q] = fmaxf(lacc.hi[q], o2f(d[3 + q])); }
+      lc += d[6];
+      if (lc == 0 || rcnt[i + 1] == 0) continue;
+      const float cost = sah_area(lacc.lo, lacc.hi) * lc + sah_area(racc[i + 1].lo, racc[i + 1].hi) * rcnt[i + 1];
+      if (cost < T.o_cost) { T.o_cost = cost; T.o_axis = k; T.o_bin = i; T.o_nl = lc; lbest = lacc; rbest = racc[i + 1]; }
+    }
+  }
+  if (spatial && T.budget > 0) {
+    float ov = 0.0f;
+    if (T.o_axis >= 0) {
+      float d[3];
+      for (int k = 0; k < 3; k++) d[k] = fmaxf(0.0f, fminf(lbest.hi[k], rbest.hi[k]) - fmaxf(lbest.lo[k], rbest.lo[k]));
+      ov = d[0] * d[1] + d[1] * d[2] + d[2] * d[0];
+    }
+    if (T.o_axis < 0 || ov > alpha * root_area) T.sp = (int32_t)atomicAdd(&counters[3], 1u);
+  }
+  task[t] = T;
+}
+
+// (2, SBVH) spatial bins of the flagged tasks: a reference enters the bin of its low end, exits the bin of
+// its high end, and adds the bounds of its clipped part to every bin it spans
+__global__ void k_sah_spbin(const uint32_t* rface, const Box6* rbox, const int32_t* ptask, const SahTask* task,
+                            const uint32_t* stat, const TriRec64* rec, int m, uint32_t* spbins) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int t = ptask[i];
+  if (t < 0 || task[t].sp < 0) return;
+  Box6 box;
+  float clo[3], ext[3];
+  task_box(stat + 12 * (size_t)t, box, clo, ext);
+  const Box6 r = rbox[i];
+  uint32_t* S = spbins + (size_t)task[t].sp * 3 * kSahBins * kSpW;
+  const TriRec64 tr = rec[rface[i]];
+  for (int k = 0; k < 3; k++) {
+    if (!((box.hi[k] - box.lo[k]) / kSahBins > 0.0f)) continue;
+    const int b0 = sp_bin(box, k, r.lo[k]), b1 = sp_bin(box, k, r.hi[k]);
+    atomicAdd(&S[(k * kSahBins + b0) * kSpW + 6], 1u);
+    atomicAdd(&S[(k * kSahBins + b1) * kSpW + 7], 1u);
+    for (int bi = b0; bi <= b1; bi++) {
+      Box6 q;
+      if (b0 == b1) q = r;
+      else if (!clip_tri(tr, k, fmaxf(sp_plane(box, k, bi), r.lo[k]), fminf(sp_plane(box, k, bi + 1), r.hi[k]), r, q)) continue;
+      uint32_t* d = S + (k * kSahBins + bi) * kSpW;
+      for (int c = 0; c < 3; c++) { atomicMin(&d[c], f2o(q.lo[c])); atomicMax(&d[3 + c], f2o(q.hi[c])); }
+    }
+  }
+}
+
+// (3) the split of every task of the level
+__global__ void k_sah_split(SahTask* task, int ntask, const uint32_t* stat, const uint32_t* spbins, const Box6* rbox,
+                            uint8_t* side, SahTask* next, uint32_t* counters, uint32_t* nchild, Box6* ncb,
+                            int leaf_size, float k_trav, int force_median) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntask) return;
+  SahTask T = task[t];
+  Box6 box;
+  float clo[3], ext[3];
+  task_box(stat + 12 * (size_t)t, box, clo, ext);
   const uint32_t n = T.count;
   const float A = fmaxf(sah_area(box.lo, box.hi), 1e-30f);
-  float best = INFINITY;
-  int axis = -1, bin = -1;
-  uint32_t nl = 0;
-  bool exact = false;  // small task: sides written here from the sorted order
+  float best = T.o_cost;
+  int axis = T.o_axis, bin = T.o_bin;
+  uint32_t nl = T.o_nl, est_l = T.o_nl, est_r = n - T.o_nl;
+  bool exact = false;
   int ord[kSahSmall];
-  if (!force_median && T.big >= 0) {
-    const uint32_t* B = bins + (size_t)T.big * 3 * kSahBins * 7;
+  if (T.sp >= 0) {  // spatial candidates: left = entries up to the plane, right = exits beyond it
+    const uint32_t* S = spbins + (size_t)T.sp * 3 * kSahBins * kSpW;
     for (int k = 0; k < 3; k++) {
-      if (!(ext[k] > 0.0f)) continue;
-      float rarea[kSahBins];
+      if (!((box.hi[k] - box.lo[k]) / kSahBins > 0.0f)) continue;
+      Box6 racc[kSahBins];
       uint32_t rcnt[kSahBins];
-      float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      Box6 acc{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
       uint32_t c = 0;
       for (int i = kSahBins - 1; i > 0; i--) {
-        const uint32_t* d = B + (k * kSahBins + i) * 7;
-        if (d[6]) for (int q = 0; q < 3; q++) { alo[q] = fminf(alo[q], o2f(d[q])); ahi[q] = fmaxf(ahi[q], o2f(d[3 + q])); }
-        c += d[6];
-        rarea[i] = c ? sah_area(alo, ahi) : 0.0f;
+        const uint32_t* d = S + (k * kSahBins + i) * kSpW;
+        if (d[0] != 0xFFFFFFFFu) for (int q = 0; q < 3; q++) { acc.lo[q] = fminf(acc.lo[q], o2f(d[q])); acc.hi[q] = fmaxf(acc.hi[q], o2f(d[3 + q])); }
+        c += d[7];
+        racc[i] = acc;
         rcnt[i] = c;
       }
-      float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      Box6 lacc{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
       uint32_t lc = 0;
       for (int i = 0; i < kSahBins - 1; i++) {
-        const uint32_t* d = B + (k * kSahBins + i) * 7;
-        if (d[6]) for (int q = 0; q < 3; q++) { llo[q] = fminf(llo[q], o2f(d[q])); lhi[q] = fmaxf(lhi[q], o2f(d[3 + q])); }
+        const uint32_t* d = S + (k * kSahBins + i) * kSpW;
+        if (d[0] != 0xFFFFFFFFu) for (int q = 0; q < 3; q++) { lacc.lo[q] = fminf(lacc.lo[q], o2f(d[q])); lacc.hi[q] = fmaxf(lacc.hi[q], o2f(d[3 + q])); }
         lc += d[6];
         if (lc == 0 || rcnt[i + 1] == 0) continue;
-        const float cost = sah_area(llo, lhi) * lc + rarea[i + 1] * rcnt[i + 1];
-        if (cost < best) { best = cost; axis = k; bin = i; nl = lc; }
+        const float cost = sah_area(lacc.lo, lacc.hi) * lc + sah_area(racc[i + 1].lo, racc[i + 1].hi) * rcnt[i + 1];
+        // a spatial split must duplicate within the budget (the estimate bounds the references it adds)
+        if (cost < best && (int64_t)lc + rcnt[i + 1] - n <= (int64_t)T.budget) {
+          best = cost; axis = 3 + k; bin = i; est_l = lc; est_r = rcnt[i + 1];
+        }
       }
     }
-  } else if (!force_median && n >= 2) {
-    // exact sweep over the centroids sorted along each axis (insertion sort by centroid, position order for ties)
+  }
+  if (!force_median && T.big < 0 && n >= 2) {
+    // exact sweep over the centroids sorted along each axis (insertion sort, position order for ties)
     Box6 pb[kSahSmall];
-    for (uint32_t j = 0; j < n; j++) pb[j] = pbox[idx[T.begin + j]];
+    for (uint32_t j = 0; j < n; j++) pb[j] = rbox[T.begin + j];
     for (int k = 0; k < 3; k++) {
       if (!(ext[k] > 0.0f)) continue;
       int o[kSahSmall];
@@ -688,115 +833,187 @@ __global__ void k_sah_split(SahTask* task, int ntask, const uint32_t* stat, cons
         o[q] = (int)j;
       }
       float rarea[kSahSmall];
-      float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      Box6 acc{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
       for (int j = (int)n - 1; j > 0; j--) {
-        for (int q = 0; q < 3; q++) { alo[q] = fminf(alo[q], pb[o[j]].lo[q]); ahi[q] = fmaxf(ahi[q], pb[o[j]].hi[q]); }
-        rarea[j] = sah_area(alo, ahi);
+        for (int q = 0; q < 3; q++) { acc.lo[q] = fminf(acc.lo[q], pb[o[j]].lo[q]); acc.hi[q] = fmaxf(acc.hi[q], pb[o[j]].hi[q]); }
+        rarea[j] = sah_area(acc.lo, acc.hi);
       }
-      float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      Box6 lacc{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
       for (uint32_t j = 0; j + 1 < n; j++) {
-        for (int q = 0; q < 3; q++) { llo[q] = fminf(llo[q], pb[o[j]].lo[q]); lhi[q] = fmaxf(lhi[q], pb[o[j]].hi[q]); }
-        const float cost = sah_area(llo, lhi) * (float)(j + 1) + rarea[j + 1] * (float)(n - 1 - j);
+        for (int q = 0; q < 3; q++) { lacc.lo[q] = fminf(lacc.lo[q], pb[o[j]].lo[q]); lacc.hi[q] = fmaxf(lacc.hi[q], pb[o[j]].hi[q]); }
+        const float cost = sah_area(lacc.lo, lacc.hi) * (float)(j + 1) + rarea[j + 1] * (float)(n - 1 - j);
         if (cost < best) {
-          best = cost; axis = k; nl = j + 1; exact = true;
+          best = cost; axis = k; nl = j + 1; exact = true; est_l = nl; est_r = n - nl;
           for (uint32_t q = 0; q < n; q++) ord[q] = o[q];
         }
       }
     }
   }
-  // the host builders' rule (rt_host.cpp BvhBuilder::build): a leaf when n <= leaf_size and no split is
-  // cheaper (or none exists, or the depth forces medians); degenerate centroids make a leaf of <= kMaxLeaf
-  // triangles; the root always splits (its handle has no parent slot)
+  // the host builders' rule: a leaf when n <= leaf_size and no split is cheaper (or none exists, or the
+  // depth forces medians); degenerate centroids make a leaf of <= kMaxLeaf; the root always splits
   const bool degenerate = !(ext[0] > 0.0f || ext[1] > 0.0f || ext[2] > 0.0f);
   bool leaf = n == 1;
   if (!leaf && (int)n <= leaf_size) leaf = force_median || axis < 0 || (float)n <= k_trav + best / A;
   if (!leaf && axis < 0 && degenerate && (int)n <= kMaxLeaf) leaf = true;
   if (T.parent_slot < 0) leaf = false;
   if (leaf) {
+    const uint32_t id = atomicAdd(&counters[4], 1u);
     T.child = -1;
+    T.bin = (int32_t)id;
     task[t] = T;
-    const uint32_t h = make_leaf(T.begin, n);
-    if (T.parent_slot >= 0) { nchild[T.parent_slot] = h; ncb[T.parent_slot] = box; }
+    nchild[T.parent_slot] = 0x80000000u | id;
+    ncb[T.parent_slot] = box;
     return;
   }
-  if (axis < 0) { bin = -1; nl = n / 2; exact = false; }  // object median by position (Morton order)
+  if (axis < 0) { axis = -1; bin = (int32_t)(n / 2); est_l = n / 2; est_r = n - n / 2; exact = false; }  // position median
   const uint32_t node = T.parent_slot < 0 ? 0u : atomicAdd(&counters[1], 1u);
   if (T.parent_slot >= 0) { nchild[T.parent_slot] = node; ncb[T.parent_slot] = box; }
   const uint32_t c = atomicAdd(&counters[0], 2u);
-  const uint32_t cnt[2] = {nl, n - nl};
+  // children's budgets: what is left after this split's estimated duplicates, in proportion to their sizes
+  const int64_t rest = (int64_t)T.budget - ((int64_t)est_l + est_r - n);
+  const int32_t bl = (int32_t)((double)rest * (double)est_l / (double)(est_l + est_r));
   for (int q = 0; q < 2; q++) {
-    SahTask C;
-    C.begin = T.begin + (q ? nl : 0);
-    C.count = cnt[q];
+    SahTask C{};
     C.parent_slot = (int32_t)(2 * node + q);
-    C.big = C.count > (uint32_t)kSahSmall ? (int32_t)atomicAdd(&counters[2], 1u) : -1;
+    C.big = -1;
+    C.sp = -1;
     C.child = -1;
     C.axis = -1;
     C.bin = -1;
-    C.nleft = 0;
-    next[c + q] = C;
+    C.budget = q ? (int32_t)(rest - bl) : bl;
+    next[c + q] = C;  // range and bin block set by k_sah_fix
   }
   T.child = (int32_t)c;
-  T.axis = exact ? -2 : axis;  // -2: sides written here
+  if (axis >= 3) T.plane = sp_plane(box, axis - 3, bin + 1);
+  T.axis = exact ? -2 : axis;
   T.bin = bin;
-  T.nleft = nl;
   task[t] = T;
-  if (exact) {
+  if (exact)
     for (uint32_t q = 0; q < n; q++) side[T.begin + ord[q]] = q < nl ? 1 : 0;
-  }
 }
 
-// (4) sides of the bin / median splits, and the scan flags (1: left side of a splitting task)
-__global__ void k_sah_side(const Box6* pbox, const uint32_t* idx, const int32_t* ptask, const SahTask* task,
-                           const uint32_t* stat, int n, uint8_t* side, uint32_t* flag) {
+// (4) sides of every position: lr = (goes left) << 32 | (goes right); fin = 1 for a finished reference
+__global__ void k_sah_side(const uint32_t* rface, const Box6* rbox, const int32_t* ptask, const SahTask* task,
+                           const uint32_t* stat, const TriRec64* rec, const uint8_t* side, int m, uint64_t* lr,
+                           uint32_t* fin) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i > m) return;
+  if (i == m) { lr[i] = 0; fin[i] = 0; return; }  // the scans' end element
   const int t = ptask[i];
-  uint32_t f = 0;
-  if (t >= 0) {
+  uint32_t L = 0, R = 0, F = 0;
+  if (t < 0) {
+    F = 1;
+  } else {
     const SahTask T = task[t];
-    if (T.child >= 0) {
-      if (T.axis >= 0) {
-        const uint32_t* s = stat + 12 * (size_t)t;
-        const float clo = o2f(s[6 + T.axis]), ext = o2f(s[9 + T.axis]) - clo;
-        f = sah_bin(cen(pbox[idx[i]], T.axis), clo, kSahBins / ext) <= T.bin ? 1u : 0u;
-      } else if (T.axis == -1) {
-        f = (uint32_t)(i - (int)T.begin) < T.nleft ? 1u : 0u;
-      } else {
-        f = side[i];
+    if (T.child < 0) {
+      F = 1;
+    } else if (T.axis >= 3) {
+      const int k = T.axis - 3;
+      const Box6 r = rbox[i];
+      if (r.hi[k] <= T.plane) L = 1;
+      else if (r.lo[k] >= T.plane) R = 1;
+      else {
+        Box6 q;
+        const TriRec64 tr = rec[rface[i]];
+        L = clip_tri(tr, k, r.lo[k], T.plane, r, q) ? 1 : 0;
+        R = clip_tri(tr, k, T.plane, r.hi[k], r, q) ? 1 : 0;
+        if (!L && !R) { if (cen(r, k) < T.plane) L = 1; else R = 1; }
       }
+    } else if (T.axis >= 0) {
+      const uint32_t* s = stat + 12 * (size_t)t;
+      const float clo = o2f(s[6 + T.axis]), ext = o2f(s[9 + T.axis]) - clo;
+      L = sah_bin(cen(rbox[i], T.axis), clo, kSahBins / ext) <= T.bin ? 1 : 0;
+      R = 1 - L;
+    } else if (T.axis == -1) {
+      L = (uint32_t)(i - (int)T.begin) < (uint32_t)T.bin ? 1 : 0;
+      R = 1 - L;
+    } else {
+      L = side[i];
+      R = 1 - L;
     }
   }
-  flag[i] = f;
+  lr[i] = ((uint64_t)L << 32) | R;
+  fin[i] = F;
 }
 
-// (5) stable partition of every splitting task's range; positions of leaves keep their place
-__global__ void k_sah_scatter(const uint32_t* idx, const int32_t* ptask, const SahTask* task, const uint32_t* flag,
-                              const uint32_t* scan, int n, uint32_t* idx_out, int32_t* ptask_out) {
+__device__ __forceinline__ uint32_t out_base(const uint64_t* slr, const uint32_t* sfin, uint32_t i) {
+  return sfin[i] + (uint32_t)(slr[i] >> 32) + (uint32_t)slr[i];
+}
+
+// (4) the child tasks' ranges (from the scans) and bin blocks
+__global__ void k_sah_fix(const SahTask* task, int ntask, const uint64_t* slr, const uint32_t* sfin, SahTask* next,
+                          uint32_t* counters) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntask) return;
+  const SahTask T = task[t];
+  if (T.child < 0) return;
+  const uint32_t b = T.begin, e = T.begin + T.count;
+  const uint32_t base = out_base(slr, sfin, b);
+  const uint32_t nL = (uint32_t)(slr[e] >> 32) - (uint32_t)(slr[b] >> 32), nR = (uint32_t)slr[e] - (uint32_t)slr[b];
+  const uint32_t cnt[2] = {nL, nR};
+  for (int q = 0; q < 2; q++) {
+    SahTask& C = next[T.child + q];
+    C.begin = base + (q ? nL : 0);
+    C.count = cnt[q];
+    C.big = cnt[q] > (uint32_t)kSahSmall ? (int32_t)atomicAdd(&counters[2], 1u) : -1;
+  }
+}
+
+// (5) the next level's references: finished ones move by the scans, a splitting task's go left then right
+// (a clipped straddler to both sides with its clipped boxes); a leaf of this level tags its references
+__global__ void k_sah_scatter(const uint32_t* rface, const Box6* rbox, const int32_t* ptask, const SahTask* task,
+                              const TriRec64* rec, const uint64_t* slr, const uint32_t* sfin, int m, uint32_t* rface_out,
+                              Box6* rbox_out, int32_t* ptask_out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= m) return;
   const int t = ptask[i];
   if (t < 0 || task[t].child < 0) {
-    idx_out[i] = idx[i];
-    ptask_out[i] = -1;
+    const uint32_t o = out_base(slr, sfin, (uint32_t)i);
+    rface_out[o] = rface[i];
+    rbox_out[o] = rbox[i];
+    ptask_out[o] = t < 0 ? t : ~task[t].bin;  // leaf id, as ~id
     return;
   }
   const SahTask T = task[t];
-  const uint32_t r = scan[i] - scan[T.begin];  // left positions of this task before i
-  const uint32_t np = flag[i] ? T.begin + r : T.begin + T.nleft + ((uint32_t)i - T.begin - r);
-  idx_out[np] = idx[i];
-  ptask_out[np] = T.child + (flag[i] ? 0 : 1);
+  const uint32_t b = T.begin, e = T.begin + T.count;
+  const uint32_t base = out_base(slr, sfin, b);
+  const uint32_t nL = (uint32_t)(slr[e] >> 32) - (uint32_t)(slr[b] >> 32);
+  const uint32_t L = (uint32_t)(slr[i + 1] >> 32) - (uint32_t)(slr[i] >> 32), R = (uint32_t)slr[i + 1] - (uint32_t)slr[i];
+  const Box6 r = rbox[i];
+  Box6 bl = r, br = r;
+  if (T.axis >= 3 && L && R) {
+    const int k = T.axis - 3;
+    const TriRec64 tr = rec[rface[i]];
+    clip_tri(tr, k, r.lo[k], T.plane, r, bl);
+    clip_tri(tr, k, T.plane, r.hi[k], r, br);
+  }
+  if (L) {
+    const uint32_t o = base + (uint32_t)(slr[i] >> 32) - (uint32_t)(slr[b] >> 32);
+    rface_out[o] = rface[i];
+    rbox_out[o] = bl;
+    ptask_out[o] = T.child;
+  }
+  if (R) {
+    const uint32_t o = base + nL + (uint32_t)slr[i] - (uint32_t)slr[b];
+    rface_out[o] = rface[i];
+    rbox_out[o] = br;
+    ptask_out[o] = T.child + 1;
+  }
 }
 }  // namespace
 
 // face_recs: one record per face (vertices = the culling bounds). Outputs: per interior node (root 0) its
 // two child handles (interior node id, or make_leaf(first slot, count)) and unpadded child boxes, and the
-// face of every triangle slot (leaves are contiguous slot ranges).
+// face of every triangle slot (leaves are contiguous slot ranges; with spatial splits a face may own
+// several slots). spatial: SBVH with duplication budget `budget` x faces and overlap threshold alpha.
 int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
-                  int leaf_size, float k_trav, std::vector<uint32_t>& nchild, std::vector<float>& ncb,
-                  std::vector<uint32_t>& slot_face, double* gpu_ms, int* levels) {
+                  int leaf_size, float k_trav, bool spatial, float budget, float alpha, std::vector<uint32_t>& nchild,
+                  std::vector<float>& ncb, std::vector<uint32_t>& slot_face, double* gpu_ms, int* levels) {
   const int n = (int)face_recs.size();
   if (n < 2) { set_error("gpu_build_sah: needs at least 2 triangles"); return RT_ERR_INVALID; }
+  const size_t N = (size_t)n;
+  const size_t cap = std::min<size_t>(spatial ? N + (size_t)(budget * (double)N) + 1 : N, (size_t)kMaxFaces);
+  if (cap < N) { set_error("gpu_build_sah: too many faces"); return RT_ERR_INVALID; }
   BCHECK(hipSetDevice(device));
   hipStream_t st;
   BCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -814,97 +1031,143 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
     if (e == hipSuccess) g.bufs.push_back(*p);
     return e;
   };
-  const size_t N = (size_t)n, maxbig = N / kSahSmall + 2, binw = 3 * kSahBins * 7;
+  const size_t maxbig = cap / kSahSmall + 2, objw = 3 * kSahBins * kObjW, spw = 3 * kSahBins * kSpW;
   TriRec64* d_rec = nullptr;
-  uint64_t *d_k0 = nullptr, *d_k1 = nullptr;
-  Box6 *d_pbox = nullptr, *d_ncb = nullptr;
-  uint32_t *d_idx[2] = {nullptr, nullptr}, *d_stat = nullptr, *d_bins = nullptr, *d_flag = nullptr, *d_scan = nullptr;
-  uint32_t *d_cnt = nullptr, *d_nchild = nullptr;
+  uint64_t *d_k0 = nullptr, *d_k1 = nullptr, *d_lr = nullptr, *d_slr = nullptr;
+  Box6 *d_rbox[2] = {nullptr, nullptr}, *d_ncb = nullptr;
+  uint32_t *d_rface[2] = {nullptr, nullptr}, *d_stat = nullptr, *d_bins = nullptr, *d_spbins = nullptr;
+  uint32_t *d_fin = nullptr, *d_sfin = nullptr, *d_cnt = nullptr, *d_nchild = nullptr;
   int32_t* d_pt[2] = {nullptr, nullptr};
   SahTask* d_task[2] = {nullptr, nullptr};
   uint8_t* d_side = nullptr;
   BCHECK(alloc((void**)&d_rec, N * sizeof(TriRec64)));
   BCHECK(alloc((void**)&d_k0, N * 8));
   BCHECK(alloc((void**)&d_k1, N * 8));
-  BCHECK(alloc((void**)&d_pbox, N * sizeof(Box6)));
-  BCHECK(alloc((void**)&d_ncb, 2 * N * sizeof(Box6)));
-  BCHECK(alloc((void**)&d_nchild, 2 * N * 4));
+  BCHECK(alloc((void**)&d_ncb, 2 * cap * sizeof(Box6)));
+  BCHECK(alloc((void**)&d_nchild, 2 * cap * 4));
   for (int q = 0; q < 2; q++) {
-    BCHECK(alloc((void**)&d_idx[q], N * 4));
-    BCHECK(alloc((void**)&d_pt[q], N * 4));
-    BCHECK(alloc((void**)&d_task[q], N * sizeof(SahTask)));
+    BCHECK(alloc((void**)&d_rface[q], cap * 4));
+    BCHECK(alloc((void**)&d_rbox[q], cap * sizeof(Box6)));
+    BCHECK(alloc((void**)&d_pt[q], cap * 4));
+    BCHECK(alloc((void**)&d_task[q], cap * sizeof(SahTask)));
   }
-  BCHECK(alloc((void**)&d_stat, N * 12 * 4));
-  BCHECK(alloc((void**)&d_bins, maxbig * binw * 4));
-  BCHECK(alloc((void**)&d_flag, N * 4));
-  BCHECK(alloc((void**)&d_scan, N * 4));
-  BCHECK(alloc((void**)&d_side, N));
-  BCHECK(alloc((void**)&d_cnt, 16));
+  BCHECK(alloc((void**)&d_stat, cap * 12 * 4));
+  BCHECK(alloc((void**)&d_bins, maxbig * objw * 4));
+  if (spatial) BCHECK(alloc((void**)&d_spbins, maxbig * spw * 4));
+  BCHECK(alloc((void**)&d_lr, (cap + 1) * 8));
+  BCHECK(alloc((void**)&d_slr, (cap + 1) * 8));
+  BCHECK(alloc((void**)&d_fin, (cap + 1) * 4));
+  BCHECK(alloc((void**)&d_sfin, (cap + 1) * 4));
+  BCHECK(alloc((void**)&d_side, cap));
+  BCHECK(alloc((void**)&d_cnt, 32));
   BCHECK(hipMemcpyAsync(d_rec, face_recs.data(), N * sizeof(TriRec64), hipMemcpyHostToDevice, st));
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
   BCHECK(hipEventCreate(&e1));
   BCHECK(hipEventRecord(e0, st));
-  const int B = kSahBlock, G = (n + B - 1) / B;
+  const int B = kSahBlock;
+  auto grid = [&](size_t k) { return dim3((unsigned)((k + B - 1) / B)); };
   float3 flo = make_float3(lo[0], lo[1], lo[2]), fsc;
   fsc.x = hi[0] > lo[0] ? 1024.0f / (hi[0] - lo[0]) : 0.0f;
   fsc.y = hi[1] > lo[1] ? 1024.0f / (hi[1] - lo[1]) : 0.0f;
   fsc.z = hi[2] > lo[2] ? 1024.0f / (hi[2] - lo[2]) : 0.0f;
-  hipLaunchKernelGGL(k_morton, dim3(G), dim3(B), 0, st, (const TriRec64*)d_rec, n, flo, fsc, d_k0);
-  size_t tb = 0, tscan = 0;
+  hipLaunchKernelGGL(k_morton, grid(N), dim3(B), 0, st, (const TriRec64*)d_rec, n, flo, fsc, d_k0);
+  size_t tb = 0, ts1 = 0, ts2 = 0;
   BCHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_k0, d_k1, n, 0, 64, st));
-  BCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, d_flag, d_scan, n, st));
+  BCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ts1, d_lr, d_slr, (int)(cap + 1), st));
+  BCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ts2, d_fin, d_sfin, (int)(cap + 1), st));
   void* d_tmp = nullptr;
-  BCHECK(alloc(&d_tmp, std::max(tb, tscan)));
+  BCHECK(alloc(&d_tmp, std::max(tb, std::max(ts1, ts2))));
   BCHECK(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb, d_k0, d_k1, n, 0, 64, st));
-  hipLaunchKernelGGL(k_sah_init, dim3(G), dim3(B), 0, st, (const uint64_t*)d_k1, (const TriRec64*)d_rec, n, d_pbox,
-                     d_idx[0], d_pt[0]);
-  SahTask root{0u, (uint32_t)n, -1, n > kSahSmall ? 0 : -1, -1, -1, -1, 0u};
+  hipLaunchKernelGGL(k_sah_init, grid(N), dim3(B), 0, st, (const uint64_t*)d_k1, (const TriRec64*)d_rec, n, d_rface[0],
+                     d_rbox[0], d_pt[0]);
+  SahTask root{};
+  root.begin = 0;
+  root.count = (uint32_t)n;
+  root.parent_slot = -1;
+  root.big = n > kSahSmall ? 0 : -1;
+  root.sp = -1;
+  root.child = -1;
+  root.axis = root.bin = -1;
+  root.budget = (int32_t)(cap - N);
   BCHECK(hipMemcpyAsync(d_task[0], &root, sizeof root, hipMemcpyHostToDevice, st));
+  float root_area;
+  {
+    const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    root_area = std::max(dx * dy + dy * dz + dz * dx, 1e-30f);
+  }
   int ntask = 1, nbig = n > kSahSmall ? 1 : 0, cur = 0, level = 0;
-  uint32_t nodes = 1;
+  uint32_t nodes = 1, leaves = 0, m = (uint32_t)n;
   const int lb = std::max(1, std::min(leaf_size, kMaxLeaf));
   while (ntask > 0) {
     if (level > 4 * kMaxDepth) { set_error("gpu_build_sah: no progress"); return RT_ERR_INVALID; }
-    // stats: lo halves start at all-ones, hi halves at 0 (ordered uints)
-    hipLaunchKernelGGL(k_sah_stat_init, dim3((ntask + 255) / 256), dim3(256), 0, st, d_stat, ntask);
-    if (nbig) hipLaunchKernelGGL(k_sah_bins_init, dim3((nbig * 3 * kSahBins + 255) / 256), dim3(256), 0, st, d_bins, nbig);
-    hipLaunchKernelGGL(k_sah_bounds, dim3(G), dim3(B), 0, st, (const Box6*)d_pbox, (const uint32_t*)d_idx[cur],
-                       (const int32_t*)d_pt[cur], n, d_stat);
-    if (nbig)
-      hipLaunchKernelGGL(k_sah_bin, dim3(G), dim3(B), 0, st, (const Box6*)d_pbox, (const uint32_t*)d_idx[cur],
-                         (const int32_t*)d_pt[cur], (const SahTask*)d_task[cur], (const uint32_t*)d_stat, n, d_bins);
-    BCHECK(hipMemsetAsync(d_cnt, 0, 16, st));
-    const uint32_t init_nodes[1] = {nodes};
-    BCHECK(hipMemcpyAsync(d_cnt + 1, init_nodes, 4, hipMemcpyHostToDevice, st));
     const int force = level >= kMaxDepth - 20 ? 1 : 0;
-    hipLaunchKernelGGL(k_sah_split, dim3((ntask + 127) / 128), dim3(128), 0, st, d_task[cur], ntask,
-                       (const uint32_t*)d_stat, (const uint32_t*)d_bins, (const Box6*)d_pbox, (const uint32_t*)d_idx[cur],
-                       d_side, d_task[1 - cur], d_cnt, d_nchild, d_ncb, lb, k_trav, force);
-    hipLaunchKernelGGL(k_sah_side, dim3(G), dim3(B), 0, st, (const Box6*)d_pbox, (const uint32_t*)d_idx[cur],
-                       (const int32_t*)d_pt[cur], (const SahTask*)d_task[cur], (const uint32_t*)d_stat, n, d_side, d_flag);
-    BCHECK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tscan, d_flag, d_scan, n, st));
-    hipLaunchKernelGGL(k_sah_scatter, dim3(G), dim3(B), 0, st, (const uint32_t*)d_idx[cur], (const int32_t*)d_pt[cur],
-                       (const SahTask*)d_task[cur], (const uint32_t*)d_flag, (const uint32_t*)d_scan, n, d_idx[1 - cur],
+    uint32_t cinit[8] = {0, nodes, 0, 0, leaves, 0, 0, 0};
+    BCHECK(hipMemcpyAsync(d_cnt, cinit, 32, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_sah_stat_init, grid(ntask), dim3(B), 0, st, d_stat, ntask);
+    if (nbig)
+      hipLaunchKernelGGL(k_sah_bins_init, grid((size_t)nbig * 3 * kSahBins), dim3(B), 0, st, d_bins, nbig * 3 * kSahBins, kObjW);
+    hipLaunchKernelGGL(k_sah_bounds, grid(m), dim3(B), 0, st, (const Box6*)d_rbox[cur], (const int32_t*)d_pt[cur], (int)m, d_stat);
+    if (nbig)
+      hipLaunchKernelGGL(k_sah_bin, grid(m), dim3(B), 0, st, (const Box6*)d_rbox[cur], (const int32_t*)d_pt[cur],
+                         (const SahTask*)d_task[cur], (const uint32_t*)d_stat, (int)m, d_bins);
+    hipLaunchKernelGGL(k_sah_split_obj, grid(ntask), dim3(B), 0, st, d_task[cur], ntask, (const uint32_t*)d_stat,
+                       (const uint32_t*)d_bins, d_cnt, root_area, alpha, spatial ? 1 : 0, force);
+    if (spatial && nbig) {
+      uint32_t nsp = 0;
+      BCHECK(hipMemcpyAsync(&nsp, d_cnt + 3, 4, hipMemcpyDeviceToHost, st));
+      BCHECK(hipStreamSynchronize(st));
+      if (nsp > maxbig) { set_error("gpu_build_sah: spatial task bound exceeded"); return RT_ERR_INVALID; }
+      if (nsp) {
+        hipLaunchKernelGGL(k_sah_bins_init, grid((size_t)nsp * 3 * kSahBins), dim3(B), 0, st, d_spbins, (int)nsp * 3 * kSahBins, kSpW);
+        hipLaunchKernelGGL(k_sah_spbin, grid(m), dim3(B), 0, st, (const uint32_t*)d_rface[cur], (const Box6*)d_rbox[cur],
+                           (const int32_t*)d_pt[cur], (const SahTask*)d_task[cur], (const uint32_t*)d_stat,
+                           (const TriRec64*)d_rec, (int)m, d_spbins);
+      }
+    }
+    hipLaunchKernelGGL(k_sah_split, grid(ntask), dim3(B), 0, st, d_task[cur], ntask, (const uint32_t*)d_stat,
+                       (const uint32_t*)d_spbins, (const Box6*)d_rbox[cur], d_side, d_task[1 - cur], d_cnt, d_nchild,
+                       d_ncb, lb, k_trav, force);
+    hipLaunchKernelGGL(k_sah_side, grid(m + 1), dim3(B), 0, st, (const uint32_t*)d_rface[cur], (const Box6*)d_rbox[cur],
+                       (const int32_t*)d_pt[cur], (const SahTask*)d_task[cur], (const uint32_t*)d_stat,
+                       (const TriRec64*)d_rec, (const uint8_t*)d_side, (int)m, d_lr, d_fin);
+    BCHECK(hipcub::DeviceScan::ExclusiveSum(d_tmp, ts1, d_lr, d_slr, (int)(m + 1), st));
+    BCHECK(hipcub::DeviceScan::ExclusiveSum(d_tmp, ts2, d_fin, d_sfin, (int)(m + 1), st));
+    hipLaunchKernelGGL(k_sah_fix, grid(ntask), dim3(B), 0, st, (const SahTask*)d_task[cur], ntask, (const uint64_t*)d_slr,
+                       (const uint32_t*)d_sfin, d_task[1 - cur], d_cnt);
+    uint64_t slr_m = 0;
+    uint32_t sfin_m = 0;
+    BCHECK(hipMemcpyAsync(&slr_m, d_slr + m, 8, hipMemcpyDeviceToHost, st));
+    BCHECK(hipMemcpyAsync(&sfin_m, d_sfin + m, 4, hipMemcpyDeviceToHost, st));
+    BCHECK(hipStreamSynchronize(st));
+    const uint32_t m_next = sfin_m + (uint32_t)(slr_m >> 32) + (uint32_t)slr_m;
+    if (m_next > cap || m_next < m) { set_error("gpu_build_sah: reference bound exceeded"); return RT_ERR_INVALID; }
+    hipLaunchKernelGGL(k_sah_scatter, grid(m), dim3(B), 0, st, (const uint32_t*)d_rface[cur], (const Box6*)d_rbox[cur],
+                       (const int32_t*)d_pt[cur], (const SahTask*)d_task[cur], (const TriRec64*)d_rec,
+                       (const uint64_t*)d_slr, (const uint32_t*)d_sfin, (int)m, d_rface[1 - cur], d_rbox[1 - cur],
                        d_pt[1 - cur]);
     BCHECK(hipGetLastError());
-    uint32_t cnt[4];
-    BCHECK(hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, st));
+    uint32_t cnt[8];
+    BCHECK(hipMemcpyAsync(cnt, d_cnt, 32, hipMemcpyDeviceToHost, st));
     BCHECK(hipStreamSynchronize(st));
     ntask = (int)cnt[0];
     nodes = cnt[1];
     nbig = (int)cnt[2];
-    if ((size_t)nbig > maxbig || nodes > N) { set_error("gpu_build_sah: task bound exceeded"); return RT_ERR_INVALID; }
+    leaves = cnt[4];
+    m = m_next;
+    if ((size_t)nbig > maxbig || nodes > cap || (size_t)ntask > cap) { set_error("gpu_build_sah: task bound exceeded"); return RT_ERR_INVALID; }
     cur = 1 - cur;
     level++;
   }
   BCHECK(hipEventRecord(e1, st));
+  std::vector<int32_t> ptag(m);
   nchild.resize(2 * (size_t)nodes);
   ncb.resize(12 * (size_t)nodes);
-  slot_face.resize(N);
+  slot_face.resize(m);
   BCHECK(hipMemcpyAsync(nchild.data(), d_nchild, 2 * (size_t)nodes * 4, hipMemcpyDeviceToHost, st));
   BCHECK(hipMemcpyAsync(ncb.data(), d_ncb, 2 * (size_t)nodes * sizeof(Box6), hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(slot_face.data(), d_idx[cur], N * 4, hipMemcpyDeviceToHost, st));
+  BCHECK(hipMemcpyAsync(slot_face.data(), d_rface[cur], (size_t)m * 4, hipMemcpyDeviceToHost, st));
+  BCHECK(hipMemcpyAsync(ptag.data(), d_pt[cur], (size_t)m * 4, hipMemcpyDeviceToHost, st));
   BCHECK(hipStreamSynchronize(st));
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
@@ -912,6 +1175,22 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   if (levels) *levels = level;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  // leaves: each leaf id's references are one contiguous run of the final order
+  std::vector<uint32_t> first(leaves, UINT32_MAX), count(leaves, 0);
+  for (uint32_t i = 0; i < m; i++) {
+    const int32_t tg = ptag[i];
+    const uint32_t id = (uint32_t)~tg;
+    if (tg >= 0 || id >= leaves) { set_error("gpu_build_sah: unfinished reference"); return RT_ERR_INVALID; }
+    if (first[id] == UINT32_MAX) first[id] = i;
+    else if (first[id] + count[id] != i) { set_error("gpu_build_sah: leaf %u not contiguous", id); return RT_ERR_INVALID; }
+    count[id]++;
+  }
+  for (uint32_t& h : nchild) {
+    if (!(h & 0x80000000u)) continue;
+    const uint32_t id = h & 0x7FFFFFFFu;
+    if (id >= leaves || count[id] == 0 || count[id] > (uint32_t)kMaxLeaf) { set_error("gpu_build_sah: bad leaf %u", id); return RT_ERR_INVALID; }
+    h = make_leaf(first[id], count[id]);
+  }
   return RT_OK;
 }
 

@@ -175,7 +175,7 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
   s->opts.min_faces = h.min_faces;
   s->opts.max_boxes = h.max_boxes;
   s->opts.leaf_size = h.leaf_size;
-  if (h.builder < RT_BUILDER_SAH || h.builder > RT_BUILDER_SAH_GPU) { rt::set_error("rt_scene_load: bad builder id in %s", path); return RT_ERR_IO; }
+  if (h.builder < RT_BUILDER_SAH || h.builder > RT_BUILDER_SBVH_GPU) { rt::set_error("rt_scene_load: bad builder id in %s", path); return RT_ERR_IO; }
   s->opts.builder = h.builder;
   s->builder_used = h.builder;
   s->opts.frames_in_flight = std::max(1, std::min(s->opts.frames_in_flight, (int32_t)rt_scene::kMaxSlots));

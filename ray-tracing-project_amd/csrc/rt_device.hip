@@ -750,7 +750,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   {
     const bool prim_mode = fr->mode == RT_MODE_PRIMARY || boxcol;
     const bool need = trav != TRAV_B2_LDS || dual || (fr->mode == RT_MODE_FULL && (variant & 16)) ||
-                      (prim_mode && !stats && (variant & (256 | 2048 | 4194304)));
+                      (prim_mode && !stats && (variant & (256 | 2048)));
     if (need && !variants_linked()) {
       set_error("rt_render: kernel variant %d is an A/B build option, not in this library (make variants)", variant);
       return RT_ERR_UNSUPPORTED;
@@ -848,11 +848,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
       // occupancy experiments (160 KiB / (pad + 1 KiB) blocks per CU)
       const char* lds_pad_env = debug_env("RT_LDS_PAD");
       const unsigned lds_pad = lds_pad_env ? (unsigned)atoi(lds_pad_env) : 0u;
-      if (variant & 4194304) {  // A/B: PRIMARY descent by the packet's frustum test (rt_variants.hip)
-        VariantCall vc;
-        vc.P = P, vc.units = (size_t)grid * (4 / kTraceWPB), vc.st = st, vc.hits = hits, vc.boxcol = boxcol;
-        variant_launch(VOP_PRIMARY_FRUSTUM, vc);
-      } else if (boxcol) {
+      if (boxcol) {
         if (hits) hipLaunchKernelGGL((k_primary_fused<true, true>), g, b, lds_pad, st, P);
         else hipLaunchKernelGGL((k_primary_fused<false, true>), g, b, lds_pad, st, P);
       } else {

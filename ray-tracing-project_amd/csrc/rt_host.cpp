@@ -557,7 +557,7 @@ extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
   o->max_boxes = INT32_MAX; // flyscene.hpp:169
   o->leaf_size = 0;
   o->frames_in_flight = 4;
-  o->builder = RT_BUILDER_SBVH;
+  o->builder = RT_BUILDER_SBVH_GPU;  // host RT_BUILDER_SBVH when there is no device
   for (int k = 0; k < 3; k++) { o->default_material.ka[k] = 0.2f; o->background[k] = 0.9f; }
   o->default_material.kd[0] = 0.9f; o->default_material.kd[1] = 0.9f; o->default_material.kd[2] = 0.0f;
   o->default_material.shininess = 0.0f;
@@ -1720,7 +1720,9 @@ bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
 // pre-order indices, every collapsed subtree / single triangle becomes a leaf whose triangles take
 // consecutive slots in depth-first order (child 0 first), and relayout_dfs re-lays out the nodes as for the
 // host builders. false (nothing changed) when the device build is impossible or the tree too deep.
-constexpr int kPlocRadius = 24;       // clusters searched either side (the paper's quality setting ~25)
+// clusters searched either side: on the C3 soup a wider search gives a worse tree (radius 4 / 16 / 32: SAH
+// cost 506 / 513 / 517, C3 8.3 / 7.0 / 6.3 Grays/s, profiles/ab/r04_builders.txt), so 4, not the paper's ~25
+constexpr int kPlocRadius = 4;
 constexpr float kPlocTrav = 0.7f;     // node-step cost relative to a triangle test (as the host builders)
 bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   if (hs.nf < 2) return false;
@@ -1814,7 +1816,7 @@ bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
 // GPU top-down binned SAH (rt_build.hip gpu_build_sah) + host layout: interior node 0 is the root, child
 // handles are node ids or leaf handles over the returned slot order; the host pads the boxes and re-lays
 // the nodes out depth first. false (nothing changed) when the device build is impossible or too deep.
-bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
+bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, double* gpu_ms) {
   if (hs.nf < 2) return false;
   float lo[3], hi[3];
   world_bounds(hs, lo, hi);
@@ -1826,8 +1828,11 @@ bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms)
   int levels = 0;
   float trav = 0.7f;
   if (const char* e = debug_env("RT_SAH_TRAV")) trav = std::max(0.05f, (float)atof(e));
-  if (gpu_build_sah(device, recs, lo, hi, std::max(1, std::min(leaf_size, kMaxLeaf)), trav, nchild, ncb, slot_face, gpu_ms,
-                    &levels) != RT_OK)
+  float budget = 0.5f;  // as the host SBVH (rt_host.cpp build_sbvh)
+  if (const char* e = debug_env("RT_SBVH_BUDGET")) budget = std::max(0.0f, (float)atof(e));
+  constexpr float kSbvhGpuAlpha = 1e-3f;  // the host SBVH's overlap threshold (build_bvh)
+  if (gpu_build_sah(device, recs, lo, hi, std::max(1, std::min(leaf_size, kMaxLeaf)), trav, spatial, budget, kSbvhGpuAlpha,
+                    nchild, ncb, slot_face, gpu_ms, &levels) != RT_OK)
     return false;
   const size_t nn = nchild.size() / 2;
   const float pad = bvh_pad(lo, hi);
@@ -1847,7 +1852,9 @@ bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms)
   HostScene trial;
   relayout_dfs(trial, tmp, 0);
   if (trial.depth > kMaxDepth + 2) return false;  // too deep for the wave stack: host SAH instead
-  if (debug_env("RT_TIMING")) fprintf(stderr, "[rt] sah-gpu: %d levels, %zu nodes, depth %d\n", levels, nn, trial.depth);
+  if (debug_env("RT_TIMING"))
+    fprintf(stderr, "[rt] %s: %d levels, %zu nodes, %zu references, depth %d\n", spatial ? "sbvh-gpu" : "sah-gpu", levels, nn,
+            slot_face.size(), trial.depth);
   std::vector<TriRec64> tris(slot_face.size());
   for (size_t sl = 0; sl < slot_face.size(); sl++) tris[sl] = recs[slot_face[sl]];
   hs.nodes = std::move(trial.nodes);
@@ -2145,11 +2152,11 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
             s->box_builder_used == RT_BOXES_GPU ? "gpu" : "host", s->boxes_gpu_ms, hs.boxes.size());
   auto t2 = clk::now();
   bool built = false;
-  if (s->opts.builder == RT_BUILDER_SAH_GPU && s->opts.device != RT_DEVICE_NONE) {
+  if ((s->opts.builder == RT_BUILDER_SAH_GPU || s->opts.builder == RT_BUILDER_SBVH_GPU) && s->opts.device != RT_DEVICE_NONE) {
     int dev = s->opts.device;
     if (dev < 0) dev = rt::current_device();
-    built = dev >= 0 && rt::build_bvh_sah_gpu(hs, dev, leaf, &s->bvh_gpu_ms);
-    if (built) s->builder_used = RT_BUILDER_SAH_GPU;
+    built = dev >= 0 && rt::build_bvh_sah_gpu(hs, dev, leaf, s->opts.builder == RT_BUILDER_SBVH_GPU, &s->bvh_gpu_ms);
+    if (built) s->builder_used = s->opts.builder;
   }
   if (s->opts.builder == RT_BUILDER_PLOC_GPU && s->opts.device != RT_DEVICE_NONE) {
     int dev = s->opts.device;
@@ -2166,8 +2173,8 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     built = dev >= 0 && rt::build_bvh_gpu(hs, dev, lb_leaf, &s->bvh_gpu_ms);
     if (built) s->builder_used = RT_BUILDER_LBVH_GPU;
   }
-  if (!built) {
-    const bool spatial = s->opts.builder == RT_BUILDER_SBVH;
+  if (!built) {  // host build: spatial splits for either SBVH builder, binned SAH for the rest
+    const bool spatial = s->opts.builder == RT_BUILDER_SBVH || s->opts.builder == RT_BUILDER_SBVH_GPU;
     rt::build_bvh(hs, leaf, spatial);
     s->builder_used = spatial ? RT_BUILDER_SBVH : RT_BUILDER_SAH;
     if (rt::debug_env("RT_TIMING")) fprintf(stderr, "[rt] build_bvh %.1f ms\n", ms_since(t2));

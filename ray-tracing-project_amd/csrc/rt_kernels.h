@@ -119,10 +119,7 @@ enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WP
        // the leaf's box (ST_WCANDM .. ST_WINSM), the triangle tests of leaves reached by descent (ST_WTRID) and
        // their entry-masked candidate count (ST_WCANDD: popped leaves unmasked), and wave-level tests where a
        // lane that never entered the leaf accepted (ST_WACCX: 0 if leaf-entry masking is exact)
-       ST_WCANDM, ST_WE1M, ST_WE2M, ST_WINSM, ST_WTRID, ST_WCANDD, ST_WACCX,
-       // RT_STATS_FRUSTUM experiment: child tests where some lane's own slab test enters but the packet's
-       // interval test does not (must stay 0: the interval test is conservative)
-       ST_WFVIOL, ST_COUNT };
+       ST_WCANDM, ST_WE1M, ST_WE2M, ST_WINSM, ST_WTRID, ST_WCANDD, ST_WACCX, ST_COUNT };
 constexpr int kStatSlots = 24;
 
 struct Hit {
@@ -394,57 +391,10 @@ template <int OCT>
 constexpr int order_bit() {
   return OCT < 6 ? OCT : OCT - 6;
 }
-// RT_STATS_FRUSTUM (counting-run experiment, ablib builds only): the closest-hit octant loops of the
-// counting run descend by a conservative wave-uniform interval test of the packet (common origin, the
-// interval of each reciprocal direction component over the wave, the wave's largest t_best) instead of
-// the union of the per-lane slab tests; triangle tests stay per lane, so the frame is unchanged and the
-// counters say how many node steps / triangle records that test visits.
-#ifndef RT_STATS_FRUSTUM
-#define RT_STATS_FRUSTUM 0
-#endif
-__device__ __forceinline__ float wave_minf(float v) {
-  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_maxf(float v) {
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
-}
-struct Frustum {
-  f3 o, idmin, idmax;
-};
-// min / max over id in [a, b] of c * id
-__device__ __forceinline__ float imul_min(float c, float a, float b) { return c >= 0.0f ? c * a : c * b; }
-__device__ __forceinline__ float imul_max(float c, float a, float b) { return c >= 0.0f ? c * b : c * a; }
-template <int OCT>
-__device__ __forceinline__ bool frustum_enter(const Frustum& F, float lx, float hx, float ly, float hy, float lz, float hz,
-                                              float T) {
-  const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
-  const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
-  const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
-  const float tn = fmaxf(fmaxf(imul_min(nx - F.o.x, F.idmin.x, F.idmax.x), imul_min(ny - F.o.y, F.idmin.y, F.idmax.y)),
-                         fmaxf(imul_min(nz - F.o.z, F.idmin.z, F.idmax.z), 0.0f));
-  const float tf = fminf(fminf(imul_max(fx - F.o.x, F.idmin.x, F.idmax.x), imul_max(fy - F.o.y, F.idmin.y, F.idmax.y)),
-                         fminf(imul_max(fz - F.o.z, F.idmin.z, F.idmax.z), T));
-  return tn <= tf;
-}
-
 template <bool ANY, bool STATS, bool STACK_LDS, int OCT = -1>
 __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                          uint32_t* lds_stack, uint32_t* cnt) {
   if (P.n_nodes == 0) return;
-  constexpr bool FRU = RT_STATS_FRUSTUM && STATS && !ANY && OCT >= 0;
-  Frustum F{};
-  bool fru = false;  // the packet has one common origin (primary rays): the interval test drives descent
-  if (FRU) {
-    const float ox = __shfl(r.o.x, (int)__builtin_ctzll(ballot(active) | (1ull << 63)), 64);
-    const float oy = __shfl(r.o.y, (int)__builtin_ctzll(ballot(active) | (1ull << 63)), 64);
-    const float oz = __shfl(r.o.z, (int)__builtin_ctzll(ballot(active) | (1ull << 63)), 64);
-    fru = ballot(active && (r.o.x != ox || r.o.y != oy || r.o.z != oz)) == 0 && ballot(active) != 0;
-    F.o = f3{ox, oy, oz};
-    F.idmin = f3{wave_minf(active ? r.id.x : INFINITY), wave_minf(active ? r.id.y : INFINITY), wave_minf(active ? r.id.z : INFINITY)};
-    F.idmax = f3{wave_maxf(active ? r.id.x : -INFINITY), wave_maxf(active ? r.id.y : -INFINITY), wave_maxf(active ? r.id.z : -INFINITY)};
-  }
   uint32_t stackv = 0;     // lane k holds stack entry k (VGPR stack)
   int sp = 0;              // wave-uniform stack depth (SGPR)
   uint64_t flagstack = 0;  // STATS: per-lane "my ray wanted this entry" bit per stack level
@@ -467,16 +417,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
       const float tcut = ANY ? tmax_any : h.t;
       const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, r, tcut);
       const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, r, tcut);
-      uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
-      const uint64_t lm0 = m0, lm1 = m1;  // the lanes' own verdicts (want flags)
-      if (FRU && fru) {
-        const float T = wave_maxf(active ? h.t : -INFINITY);
-        const bool f0 = frustum_enter<OCT>(F, nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, T);
-        const bool f1 = frustum_enter<OCT>(F, nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, T);
-        cnt[ST_WFVIOL] += (m0 != 0 && !f0) + (m1 != 0 && !f1);
-        m0 = f0 ? ~0ull : 0ull;
-        m1 = f1 ? ~0ull : 0ull;
-      }
+      const uint64_t m0 = mask_le(s0.tmin, s0.tmax) & act, m1 = mask_le(s1.tmin, s1.tmax) & act;
       bool first0;
       if (OCT >= 0) {
         // the node's order bit for this octant, overridden when only one child is needed
@@ -496,7 +437,7 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
                         : "s"(uniform(far)), "s"(uniform((uint32_t)sp))
                         : "m0");
       if (STATS) {
-        const bool h0 = (lm0 >> lane_id()) & 1, h1 = (lm1 >> lane_id()) & 1;
+        const bool h0 = (m0 >> lane_id()) & 1, h1 = (m1 >> lane_id()) & 1;
         const bool wf = first0 ? h1 : h0;
         flagstack = (flagstack & ~(1ull << sp)) | ((uint64_t)wf << sp);
         want = first0 ? h0 : h1;
@@ -1675,7 +1616,6 @@ enum VariantOp {
   VOP_PRIMARY_X2,         // two rays per lane (variant bit 256)
   VOP_PRIMARY_PERSISTENT, // persistent threads (variant bit 2048; 4096: no stealing)
   VOP_RAYS,               // ray-list queries with a non-default traversal flavour
-  VOP_PRIMARY_FRUSTUM,    // PRIMARY descent by the packet's frustum test (variant bit 4194304)
 };
 struct VariantCall {
   FrameParams P;

@@ -76,9 +76,9 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
                    int leaf_size, int radius, float k_trav, std::vector<int32_t>& child2, std::vector<float>& box6,
                    std::vector<uint8_t>& leaf, double* gpu_ms, int* iterations, int rule);
 int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
-                  int leaf_size, float k_trav, std::vector<uint32_t>& nchild, std::vector<float>& ncb,
-                  std::vector<uint32_t>& slot_face, double* gpu_ms, int* levels);
-bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms);
+                  int leaf_size, float k_trav, bool spatial, float budget, float alpha, std::vector<uint32_t>& nchild,
+                  std::vector<float>& ncb, std::vector<uint32_t>& slot_face, double* gpu_ms, int* levels);
+bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, double* gpu_ms);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
 void build_bvh4(HostScene& hs);

@@ -808,178 +808,6 @@ __global__ __launch_bounds__(256) void k_full_final(FrameParams P) {
 
 
 // ------------------------------------------------------------------------------------------------
-// Frustum-descent PRIMARY traversal (variant bit 4194304): a packet of primary rays shares one origin
-// (the eye), so whether SOME ray of the wave can enter a child box is decided by one conservative interval
-// test of the packet instead of 64 per-lane slab tests: with the interval [idmin_k, idmax_k] of each
-// reciprocal direction component over the wave, the earliest entry through a near plane c is
-// min over id of (c - o) * id and the latest exit through a far plane max over id -- both at an interval
-// end chosen by the sign of (c - o). The twelve planes of a node's two children are evaluated in twelve
-// lanes at once (one vector load of the plane coordinates, four VALU), reduced per child with quad DPP
-// maxima (far planes negated), and compared with the wave's largest t_best. Visiting a superset of the
-// per-lane union is exact: every lane still tests every triangle of every visited leaf with the
-// reference's arithmetic. Non-primary packets (mixed origins / octants, uncertified rays) take the
-// product loops.
-// ------------------------------------------------------------------------------------------------
-struct FrustumLanes {
-  uint32_t field;  // byte offset of this lane's plane coordinate within the 64-B node record
-  float off;       // -(o_k +- p): d = c + off = (c -+ p) - o_k, the plane grown by the ray pad
-  float A, B;      // t = d >= 0 ? d * A : d * B (far planes negated; the clip lane: 0)
-};
-
-__device__ __forceinline__ float dpp_quad_max(float v) {
-  // max over the lane's quad: quad_perm [1,0,3,2] then [2,3,0,1]
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
-  return v;
-}
-
-// the per-wave set-up: false when the packet is not a common-origin, certified one (then the caller
-// walks it with the product loop)
-template <int OCT>
-__device__ __forceinline__ bool frustum_setup(const Ray& r, bool active, float static_pad, FrustumLanes& F) {
-  const uint64_t act = ballot(active);
-  if (act == 0) return false;
-  const int first = (int)__builtin_ctzll(act);
-  const float ox = __shfl(r.o.x, first, 64), oy = __shfl(r.o.y, first, 64), oz = __shfl(r.o.z, first, 64);
-  if (ballot(active && (r.o.x != ox || r.o.y != oy || r.o.z != oz)) != 0) return false;
-  // the ray pad of setup_cull: a function of the (common) origin; unbounded boxes (uncertified rays) and
-  // non-finite reciprocals: not this loop
-  const float om = fmaxf(fmaxf(fabsf(ox), fabsf(oy)), fabsf(oz));
-  if (ballot(active && !(fabsf(r.oa.x) < INFINITY && fabsf(r.oa.y) < INFINITY && fabsf(r.oa.z) < INFINITY &&
-                         fabsf(r.id.x) < INFINITY && fabsf(r.id.y) < INFINITY && fabsf(r.id.z) < INFINITY)) != 0)
-    return false;
-  const float pr = 4e-5f * om;  // setup_cull's kCullPadRel
-  const float p = pr > static_pad ? pr : 0.0f;
-  const float mnx = wave_minf(active ? r.id.x : INFINITY), mxx = wave_maxf(active ? r.id.x : -INFINITY);
-  const float mny = wave_minf(active ? r.id.y : INFINITY), mxy = wave_maxf(active ? r.id.y : -INFINITY);
-  const float mnz = wave_minf(active ? r.id.z : INFINITY), mxz = wave_maxf(active ? r.id.z : -INFINITY);
-  const int l = lane_id() & 15, c = l >> 3, q = l & 7;
-  const bool nearp = q < 4;
-  const int a = (q == 3 || q == 7) ? 0 : (q < 3 ? q : q - 4);
-  const bool neg = (OCT >> a) & 1;
-  const bool hi = nearp ? neg : !neg;  // a negative axis enters through its hi plane
-  F.field = 4u * (uint32_t)(6 * c + 2 * a + (hi ? 1 : 0));
-  const float oa = a == 0 ? ox : (a == 1 ? oy : oz);
-  F.off = hi ? -(oa - p) : -(oa + p);
-  const float mn = a == 0 ? mnx : (a == 1 ? mny : mnz), mx = a == 0 ? mxx : (a == 1 ? mxy : mxz);
-  if (q == 3) { F.A = 0.0f; F.B = 0.0f; }          // the entry clip at t = 0
-  else if (nearp) { F.A = mn; F.B = mx; }          // min over id of d * id
-  else { F.A = -mx; F.B = -mn; }                   // -(max over id of d * id); lane 7 repeats x
-  return true;
-}
-
-template <int OCT>
-__device__ __forceinline__ void traverse_frustum(const DevScene& P, const Ray& r, bool active, Hit& h,
-                                                 uint32_t* lds_stack, const FrustumLanes& F) {
-  if (!active) h.t = -1.0f;
-  uint64_t act = ~0ull;
-  bool found = false;
-  uint32_t node = P.root;
-  int sp = 0;
-  uint32_t cpf0 = 0, cpf1 = 0;
-  f3 rid = r.id;
-  const uint64_t bb = (uint64_t)P.nodes;
-  const uint64_t bs = ((uint64_t)uniform((uint32_t)(bb >> 32)) << 32) | (uint32_t)uniform((uint32_t)bb);
-  float T = INFINITY;  // the wave's largest t_best (an upper bound: refreshed after every leaf)
-  for (;;) {
-    while (!is_leaf(node)) {
-      const uint32_t off = node_offset(uniform(node));
-      // the twelve plane coordinates into their lanes (vector load), the record into SGPRs (scalar load)
-      float cv;
-      {
-        const uint64_t nb = bs + off;
-        const uint64_t nbs = ((uint64_t)uniform((uint32_t)(nb >> 32)) << 32) | (uint32_t)uniform((uint32_t)nb);
-        asm volatile("global_load_dword %0, %1, %2" : "=v"(cv) : "v"(F.field), "s"(nbs) : "memory");
-      }
-      const Node64 nd = sload_node_pf_inreg(P.nodes, node, cpf0, cpf1, rid);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(cv) :: "memory");
-      uint32_t nearb = 0, farb = 0;
-      sp = (int)uniform((uint32_t)sp);
-      asm("s_bitcmp1_b32 %[bits], %[oct]\n\t"
-          "s_cselect_b32 %[nb], %[c1], %[c0]\n\t"
-          "s_cselect_b32 %[fb], %[c0], %[c1]"
-          : [nb] "=&s"(nearb), [fb] "=&s"(farb)
-          : [bits] "s"(uniform(order_word<OCT>(nd))), [oct] "i"(order_bit<OCT>()), [c0] "s"(uniform(nd.child0)),
-            [c1] "s"(uniform(nd.child1))
-          : "scc");
-      lds_push(lds_stack + sp, farb);
-      const float d = cv + F.off;
-      float t = d >= 0.0f ? d * F.A : d * F.B;
-      t = dpp_quad_max(t);  // lanes 0-3 / 8-11: entry max(n_x, n_y, n_z, 0); lanes 4-7 / 12-15: -exit
-      const float sum = t + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0x114, 0xF, 0xF, false));
-      // lanes 4 / 12: entry - exit <= 0 (exact sign); lanes 0 / 8: entry <= T
-      const uint64_t mx = ballot(sum <= 0.0f), mt = ballot(t <= T);
-      const uint64_t e = (mx >> 4) & mt;
-      const uint64_t m0 = (e & 1ull) ? ~0ull : 0ull, m1 = (e & 0x100ull) ? ~0ull : 0ull;
-      sp = (int)uniform((uint32_t)sp);
-      const uint32_t c0 = uniform(nd.child0), c1 = uniform(nd.child1);
-      uint32_t nxt, ta;
-      uint64_t tt;
-      asm("s_cmp_lg_u64 %[m1], 0\n\t"
-          "s_cselect_b32 %[nxt], %[c1], -1\n\t"
-          "s_cselect_b32 %[ta], %[nb], %[c0]\n\t"
-          "s_cselect_b64 %[tt], %[m0], 0\n\t"
-          "s_cmp_lg_u64 %[m0], 0\n\t"
-          "s_cselect_b32 %[nxt], %[ta], %[nxt]\n\t"
-          "s_cmp_lg_u64 %[tt], 0\n\t"
-          "s_addc_u32 %[sp], %[sp], 0"
-          : [nxt] "=&s"(nxt), [sp] "+s"(sp), [tt] "=&s"(tt), [ta] "=&s"(ta)
-          : [m0] "s"(m0), [m1] "s"(m1), [c0] "s"(c0), [c1] "s"(c1), [nb] "s"(nearb)
-          : "scc");
-      node = nxt;
-    }
-    if (node != kPopMarker) {
-      const uint32_t first = leaf_first(node), count = leaf_count(node);
-      for (uint32_t k = 0; k < count; k++) {
-        const TriRec64 tr = sload_tri(P.tris, first + k);
-        test_tri<false>(P, tr, first + k, r, act, h, found);
-      }
-      T = wave_maxf(h.t);  // lanes without a ray carry -1, below every active lane's t_best
-    }
-    if (sp == 0) break;
-    sp--;
-    node = uniform(lds_stack[sp]);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(cpf0), "s"(cpf1) : "memory");
-  if (!active) h.t = INFINITY;
-}
-
-template <bool HITS, bool BOXCOL = false>
-__global__ __launch_bounds__(64 * kTraceWPB) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerEu)))
-void k_primary_frustum(FrameParams P) {
-  __shared__ WaveLds<TRAV_B2_LDS, false> lds;
-  wave_clock_start(P, lds.clk);
-  const PixelCoord c = pixel_coord<kTraceWPB>(P);
-  Ray r = primary_ray(P, c.px, c.py);
-  asm("" : "+v"(r.o.x), "+v"(r.o.y), "+v"(r.o.z));
-  Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  const uint64_t act = ballot(c.active);
-  const uint64_t sx = ballot(__float_as_uint(r.id.x) >> 31) & act, sy = ballot(__float_as_uint(r.id.y) >> 31) & act,
-                 sz = ballot(__float_as_uint(r.id.z) >> 31) & act;
-  bool done = false;
-  if (P.sc.n_nodes > 0 && (sx == 0 || sx == act) && (sy == 0 || sy == act) && (sz == 0 || sz == act)) {
-    const int oct = (sx ? 1 : 0) | (sy ? 2 : 0) | (sz ? 4 : 0);
-    FrustumLanes F;
-    uint32_t* st = lds.stack[c.slot];
-#define RT_FRU_CASE(o)                                                            \
-  case o:                                                                         \
-    if (frustum_setup<o>(r, c.active, P.sc.static_pad, F)) {                      \
-      traverse_frustum<o>(P.sc, r, c.active, h, st, F);                           \
-      done = true;                                                                \
-    }                                                                             \
-    break;
-    switch (oct) {
-      RT_FRU_CASE(0) RT_FRU_CASE(1) RT_FRU_CASE(2) RT_FRU_CASE(3)
-      RT_FRU_CASE(4) RT_FRU_CASE(5) RT_FRU_CASE(6) default: RT_FRU_CASE(7)
-    }
-#undef RT_FRU_CASE
-  }
-  if (!done) trace_closest_oct<false, TRAV_B2_LDS>(P.sc, r, c.active, h, lds, c.slot, nullptr);
-  if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
-  wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
-}
-
-// ------------------------------------------------------------------------------------------------
 // Host side of the variants
 // ------------------------------------------------------------------------------------------------
 template <bool STATS>
@@ -1074,17 +902,6 @@ int variant_launch(int op, const VariantCall& c) {
       // 4096: no stealing (each XCD's waves finish its own range; needs every XCD to get waves)
       hipLaunchKernelGGL(k_trace_primary_persistent, dim3(std::max(waves, 8)), dim3(64), 0, c.st, P, c.queue,
                          (c.variant & 4096) ? 0u : 7u);
-      break;
-    }
-    case VOP_PRIMARY_FRUSTUM: {
-      const dim3 g((unsigned)c.units + 3u * (unsigned)P.split_k), b(64 * kTraceWPB);
-      if (c.boxcol) {
-        if (c.hits) hipLaunchKernelGGL((k_primary_frustum<true, true>), g, b, 0, c.st, P);
-        else hipLaunchKernelGGL((k_primary_frustum<false, true>), g, b, 0, c.st, P);
-      } else {
-        if (c.hits) hipLaunchKernelGGL((k_primary_frustum<true, false>), g, b, 0, c.st, P);
-        else hipLaunchKernelGGL((k_primary_frustum<false, false>), g, b, 0, c.st, P);
-      }
       break;
     }
     case VOP_RAYS:

@@ -285,11 +285,11 @@ class Mesh:
             self.h = None
 
 
-RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH, RT_BUILDER_PLOC_GPU, RT_BUILDER_SAH_GPU = 0, 1, 2, 3, 4
+RT_BUILDER_SAH, RT_BUILDER_LBVH_GPU, RT_BUILDER_SBVH, RT_BUILDER_PLOC_GPU, RT_BUILDER_SAH_GPU, RT_BUILDER_SBVH_GPU = 0, 1, 2, 3, 4, 5
 RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 
-def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=2,
+def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=5,
                box_builder=0, wide_tree=0):
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
@@ -307,7 +307,7 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, backgr
 
 
 class Scene:
-    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=2,
+    def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=5,
                  box_builder=0, wide_tree=0, shape_model_matrix=None):
         """shape_model_matrix: the desc's getShapeModelMatrix() override (column-major 4x4), e.g. the oracle's
         after Mesh.set_model; default the loader's normalisation."""

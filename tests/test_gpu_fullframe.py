@@ -220,13 +220,13 @@ def test_gpu_lbvh_soup_matches_oracle_digests(rt, scenes):
     assert sha(face) == DIG["C3"]["face_sha256"] and sha(t) == DIG["C3"]["t_sha256"]
 
 
-@pytest.mark.parametrize("case,builder", [("C2", "ploc"), ("C3", "ploc"), ("C5", "ploc"), ("C3", "sahgpu"), ("C5", "sahgpu")])
+@pytest.mark.parametrize("case,builder", [("C2", "ploc"), ("C3", "ploc"), ("C5", "ploc"), ("C3", "sahgpu"), ("C3", "sbvhgpu"), ("C5", "sbvhgpu")])
 def test_gpu_ploc_frames_match_oracle_digests(rt, scenes, case, builder):
     """f2 PLOC and the device binned SAH on the BASELINE configs: the device-built tree's full 1080p frames
     (C2 bunny PRIMARY, C3 soup PRIMARY, C5 bunny FULL) have the oracle's face / t digests."""
     d = DIG[case]
     mesh = scenes["bunny_mesh"] if d["scene"] == "bunny" else scenes["soup_mesh"]
-    bid = rt.RT_BUILDER_PLOC_GPU if builder == "ploc" else rt.RT_BUILDER_SAH_GPU
+    bid = {"ploc": rt.RT_BUILDER_PLOC_GPU, "sahgpu": rt.RT_BUILDER_SAH_GPU, "sbvhgpu": rt.RT_BUILDER_SBVH_GPU}[builder]
     pl = rt.Scene(mesh, builder=bid)
     assert pl.info()["builder"] == bid
     rgb, face, t = gpu_frame(rt, pl, d["W"], d["H"], d["mode"])

@@ -99,7 +99,8 @@ def test_bunny_1080p(rt, orc, mode):
 @pytest.fixture(scope="module")
 def soup(rt, orc):
     mesh, v, f = rt.soup_mesh(1_000_000)
-    sc = rt.Scene(mesh)
+    # the host SBVH tree (also the quantised 4-wide tree of the W4 variant); device builders are compared with it
+    sc = rt.Scene(mesh, builder=rt.RT_BUILDER_SBVH)
     osc = orc.Scene(orc.Mesh.from_arrays(v, f, np.array([rt.SOUP_MATERIAL], np.float32)))
     return sc, osc
 
@@ -206,7 +207,7 @@ VARIANTS = {"xcd-order": 4, "xcd-runs-4": 512, "dispatch-order": 1536, "full-8-w
 # the A/B kernels of the variants library only (rt_variants.hip, `make variants`)
 VARIANTS_LIB = {"vgpr-stack": 1, "wide4": 2, "full-pipeline": 16, "pipeline-lane-refl": 48,
                 "pipeline-lane-all": 16 | 32 | 64 | 128, "two-rays-per-lane": 256, "persistent": 2048,
-                "persistent-no-steal": 2048 | 4096, "dual-chain": 1048576, "frustum-descent": 4194304}
+                "persistent-no-steal": 2048 | 4096, "dual-chain": 1048576}
 
 
 def variant_frames_identical(rt, scenes, bits):
@@ -401,13 +402,13 @@ def test_gpu_lbvh_builder(rt, soup, name):
             assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (name, m)
 
 
-@pytest.mark.parametrize("builder", ["ploc", "sahgpu"])
+@pytest.mark.parametrize("builder", ["ploc", "sahgpu", "sbvhgpu"])
 @pytest.mark.parametrize("name", ["bunny", "soup", "cube"])
 def test_gpu_ploc_builder(rt, soup, name, builder):
     """f2 "LBVH/PLOC" and the device binned SAH (rt_build.hip) give a sound tree -- every triangle inside every
     ancestor box, every face in exactly one leaf, leaves of at most 4 triangles -- and the frame of the
     host-SBVH scene bit for bit (PRIMARY and FULL); the 12-triangle cube takes the small-task paths only."""
-    bid = rt.RT_BUILDER_PLOC_GPU if builder == "ploc" else rt.RT_BUILDER_SAH_GPU
+    bid = {"ploc": rt.RT_BUILDER_PLOC_GPU, "sahgpu": rt.RT_BUILDER_SAH_GPU, "sbvhgpu": rt.RT_BUILDER_SBVH_GPU}[builder]
     if name == "cube":
         mesh = rt.Mesh.load_obj(scene_path("cube.obj"))
         ref = rt.Scene(mesh)
@@ -425,7 +426,12 @@ def test_gpu_ploc_builder(rt, soup, name, builder):
     assert info["builder"] == bid and info["bvh_gpu_ms"] > 0
     assert info["bvh_depth"] <= 62
     v = pl.validate_bvh()
-    assert v["ok"] and v["covered2"] == info["n_faces"], v
+    # spatial splits reference a straddling face from several leaves: the validator's split-aware check (every
+    # reference's clipped box inside its ancestors, every face covered) instead of one leaf per face
+    if builder == "sbvhgpu":
+        assert v["ok"] and v["covered2"] >= info["n_faces"], v
+    else:
+        assert v["ok"] and v["covered2"] == info["n_faces"], v
     cam = rt.flycam(W, H, 0, 0, 20)
     for m in (rt.RT_MODE_PRIMARY, rt.RT_MODE_FULL):
         a = ref.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)

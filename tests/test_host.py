@@ -576,11 +576,12 @@ def test_face_limit_rejected_before_reading(rt):
 
 
 def test_builder_selected_through_abi(rt, tmp_path):
-    """the host tree's builder is a scene option (RT_BUILDER_SBVH default, RT_BUILDER_SAH
-    on request), reported in rt_scene_info and kept by the scene cache -- no environment variable."""
+    """the tree's builder is a scene option (RT_BUILDER_SBVH_GPU default, which a host-only
+    scene builds as RT_BUILDER_SBVH; RT_BUILDER_SAH on request), reported in rt_scene_info and kept by the
+    scene cache -- no environment variable."""
     o = rt.SceneOpts()
     rt.lib().rt_scene_opts_default(rt.C.byref(o))
-    assert o.builder == rt.RT_BUILDER_SBVH and o.wide_tree == 0
+    assert o.builder == rt.RT_BUILDER_SBVH_GPU and o.wide_tree == 0
     mesh = _soup(rt, 20_000)
     sb = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
     sa = rt.Scene(mesh, device=rt.RT_DEVICE_NONE, builder=rt.RT_BUILDER_SAH)

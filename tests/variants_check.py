@@ -18,9 +18,11 @@ from test_gpu_parity import VARIANTS_LIB, variant_frames_identical  # noqa: E402
 def main():
     rt = conftest.rtamd
     assert os.path.basename(rt.LIB_PATH).startswith("librtamd_variants"), rt.LIB_PATH
-    bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")))
+    # host SBVH scenes: they also carry the quantised 4-wide tree the W4 variant walks (the device builders
+    # build the binary tree only, and a variant without its tree would render with the default kernels)
+    bunny = rt.Scene(rt.Mesh.load_obj(scene_path("bunny.obj")), builder=rt.RT_BUILDER_SBVH)
     mesh, _, _ = rt.soup_mesh(1_000_000)
-    soup = rt.Scene(mesh)
+    soup = rt.Scene(mesh, builder=rt.RT_BUILDER_SBVH)
     out = {}
     for name, bits in sorted(VARIANTS_LIB.items()):
         out[name] = [list(map(int, c)) for c in variant_frames_identical(rt, (bunny, soup), bits)]

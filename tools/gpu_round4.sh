@@ -34,7 +34,7 @@ for s in $STEPS; do
     builders)
       # the same C3 line per builder (SBVH default, host binned SAH, device LBVH) and PLOC radii
       export RTAMD_DEBUG_KNOBS=1
-      for cfg in ${BUILDERS:-sbvh sah sahgpu lbvh ploc:4 ploc:8 ploc:12 ploc:16}; do
+      for cfg in ${BUILDERS:-sbvh sah sahgpu sbvhgpu lbvh ploc:4}; do
         IFS=: read b r <<< "$cfg"
         RT_PLOC_RADIUS=${r:-24} timeout -k 10 120 python bench.py --steps 20 --warmup 5 --builder $b --no-cpu --no-side \
             --no-extra > $OUT/builder_$cfg.json 2> $OUT/builder_$cfg.err

@@ -15,7 +15,7 @@ NAMES = ["node_visits", "tri_tests", "wave_node_fetches", "wave_tri_fetches", "p
          "total_rays", "wave_pops", "wave_pops_cullable", "wave_wide_fetches", "wave_tri_cand", "wave_tri_prebox",
          "wave_tri_inside", "wave_tri_exit_edge1", "wave_tri_exit_edge2",
          "wave_tri_cand_m", "wave_tri_exit_edge1_m", "wave_tri_exit_edge2_m", "wave_tri_inside_m",
-         "wave_tri_desc", "wave_tri_cand_desc_m", "wave_tri_accept_outside_entry", "wave_frustum_violations"]
+         "wave_tri_desc", "wave_tri_cand_desc_m", "wave_tri_accept_outside_entry"]
 
 
 def main(scenes):
