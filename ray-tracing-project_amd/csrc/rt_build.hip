@@ -538,7 +538,11 @@ __device__ __forceinline__ float sah_area(const float* lo, const float* hi) {
   const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
   return dx * dy + dy * dz + dz * dx;
 }
-__device__ __forceinline__ int sah_bin(float c, float lo, float sc) { return min(kSahBins - 1, (int)((c - lo) * sc)); }
+// bin index, clamped explicitly (a NaN or out-of-range product lands in bin 0 / the last bin, never outside)
+__device__ __forceinline__ int sah_bin(float c, float lo, float sc) {
+  const float x = (c - lo) * sc;
+  return x >= 1.0f ? (x < (float)kSahBins ? (int)x : kSahBins - 1) : 0;
+}
 __device__ __forceinline__ bool is_lo_word(int k) { return k < 3 || (k >= 6 && k < 9); }
 
 // spatial bin planes of a task box on axis k: pl(i) = lo + w * i, pl(kSahBins) = hi (as the host builder)
@@ -547,8 +551,8 @@ __device__ __forceinline__ float sp_plane(const Box6& b, int k, int i) {
   return i >= kSahBins ? b.hi[k] : b.lo[k] + w * i;
 }
 __device__ __forceinline__ int sp_bin(const Box6& b, int k, float x) {
-  const float w = (b.hi[k] - b.lo[k]) / kSahBins;
-  int bi = min(kSahBins - 1, max(0, (int)((x - b.lo[k]) / w)));
+  const float w = (b.hi[k] - b.lo[k]) / kSahBins, q = (x - b.lo[k]) / w;
+  int bi = q >= 1.0f ? (q < (float)kSahBins ? (int)q : kSahBins - 1) : 0;
   while (bi > 0 && x < sp_plane(b, k, bi)) bi--;
   while (bi < kSahBins - 1 && x >= sp_plane(b, k, bi + 1)) bi++;
   return bi;

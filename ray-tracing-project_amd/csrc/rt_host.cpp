@@ -1453,6 +1453,16 @@ static void bound_records(const HostScene& hs, std::vector<TriRec64>& recs) {
   if (hs.av.empty()) return;
   for (TriRec64& r : recs) set_verts(r, bound_vert(hs, r.face, 0), bound_vert(hs, r.face, 1), bound_vert(hs, r.face, 2));
 }
+// the device builders take scenes whose culling bounds are finite and well inside the float range (their
+// bin arithmetic, Morton codes and surface areas stay finite); anything else is built on the host
+static bool device_buildable(const std::vector<TriRec64>& recs) {
+  for (const TriRec64& r : recs) {
+    const float v[9] = {r.w0x, r.w0y, r.w0z, r.w1x, r.w1y, r.w1z, r.w2x, r.w2y, r.w2z};
+    for (float x : v)
+      if (!(std::fabs(x) <= 1e30f)) return false;  // NaN fails too
+  }
+  return true;
+}
 static void world_records(HostScene& hs) {
   if (hs.av.empty()) return;
   for (TriRec64& r : hs.tris) {
@@ -1698,6 +1708,7 @@ bool build_bvh_gpu(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   std::vector<TriRec64> recs;
   face_records(hs, recs);
   bound_records(hs, recs);
+  if (!device_buildable(recs)) return false;
   std::vector<Node64> tmp;
   std::vector<TriRec64> tris;
   if (gpu_build_lbvh(device, recs, lo, hi, std::max(1, std::min(leaf_size, kMaxLeaf)), bvh_pad(lo, hi), tmp, tris,
@@ -1731,6 +1742,7 @@ bool build_bvh_ploc(HostScene& hs, int device, int leaf_size, double* gpu_ms) {
   std::vector<TriRec64> recs;
   face_records(hs, recs);
   bound_records(hs, recs);
+  if (!device_buildable(recs)) return false;
   std::vector<int32_t> child;
   std::vector<float> box;
   std::vector<uint8_t> leaf;
@@ -1823,6 +1835,7 @@ bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, d
   std::vector<TriRec64> recs;
   face_records(hs, recs);
   bound_records(hs, recs);
+  if (!device_buildable(recs)) return false;
   std::vector<uint32_t> nchild, slot_face;
   std::vector<float> ncb;
   int levels = 0;
