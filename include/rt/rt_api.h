@@ -402,8 +402,10 @@ int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float* cert_origi
  * PRIMARY as trace + shade kernels, 65536 the generic traceRay kernel, 131072 / 262144 / 524288
  * longest-first dispatch knobs, 2097152 PRIMARY packets on the binary tree. Bits of the variants library
  * only (make variants -> librtamd_variants.so; the product library's rt_render returns
- * RT_ERR_UNSUPPORTED for them): 1 VGPR wave stack, 2 4-wide quantised BVH, 16 FULL as a stage pipeline
- * (+32/64/128 per-lane traversal in its reflection / secondary-shadow / primary-shadow stages), 256 two
+ * RT_ERR_UNSUPPORTED for them): 1 VGPR wave stack, 2 4-wide quantised BVH (scenes of the host builders,
+ * which also build that tree), 16 FULL as a stage pipeline (whole frames only: a sharded frame returns
+ * RT_ERR_UNSUPPORTED) (+32/64/128 per-lane traversal in its reflection / secondary-shadow / primary-shadow
+ * stages), 256 two
  * rays per lane, 2048 persistent threads (+4096 no stealing), 1048576 two packets per wave. Every
  * variant renders the same bits. Returns the previous value. */
 int rt_debug_set_variant(int32_t v);

@@ -27,6 +27,18 @@ def main():
     for name, bits in sorted(VARIANTS_LIB.items()):
         out[name] = [list(map(int, c)) for c in variant_frames_identical(rt, (bunny, soup), bits)]
         print(f"{name}: {'identical' if not out[name] else out[name]}", file=sys.stderr, flush=True)
+    # the FULL stage pipeline (variant 16) sizes its ray lists for whole frames: a sharded frame is refused
+    # with an error, never rendered wrong
+    prev = rt.set_variant(16)
+    try:
+        cam = rt.flycam(256, 256, 0, 0, 20)
+        try:
+            bunny.render(cam, rt.DEFAULT_LIGHTS, 256, 256, mode=rt.RT_MODE_FULL, shard=(0, 2))
+            out["_pipeline_shard_refused"] = [[0]]
+        except rt.RTError as e:
+            out["_pipeline_shard_refused"] = [] if "whole frames only" in str(e) else [[1]]
+    finally:
+        rt.set_variant(prev)
     print(json.dumps(out), flush=True)
 
 
