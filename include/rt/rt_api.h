@@ -118,8 +118,9 @@ typedef struct rt_scene_opts {
                              * binned-SAH algorithm run top-down on the device, one level per round of
                              * launches; same fallback) or RT_BUILDER_SBVH_GPU (the same with the host
                              * SBVH's spatial splits; same fallback) */
-  int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_HOST (default,
-                             * parallel passes on the host) or RT_BOXES_GPU (one launch per pass,
+  int32_t box_builder;      /* the reference box partition (generateBoundingBoxes): RT_BOXES_GPU (default since
+                             * round 4; host-only scenes use the host builder) or RT_BOXES_HOST (parallel
+                             * passes on the host); RT_BOXES_GPU (one launch per pass,
                              * one workgroup per box; identical boxes and face order; scenes with
                              * non-finite vertex coordinates use the host builder) */
   int32_t wide_tree;        /* 1: also build the fp32 4-wide tree (eight per-octant copies of 128-B nodes in

@@ -330,7 +330,7 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   BCHECK(alloc((void**)&d_pbox, (size_t)n * sizeof(Box6)));
   BCHECK(alloc((void**)&d_nbox, (size_t)n * sizeof(Box6)));
   BCHECK(alloc((void**)&d_nodes, (size_t)n * sizeof(Node64)));
-  BCHECK(hipMemcpyAsync(d_rec, face_recs.data(), (size_t)n * sizeof(TriRec64), hipMemcpyHostToDevice, st));
+  if (int rc = h2d(d_rec, face_recs.data(), (size_t)n * sizeof(TriRec64))) return rc;  // pinned staging
   BCHECK(hipMemsetAsync(d_flags, 0, (size_t)n * 4, st));
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
@@ -358,9 +358,9 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   BCHECK(hipEventRecord(e1, st));
   nodes.resize((size_t)n - 1);
   tris.resize(n);
-  BCHECK(hipMemcpyAsync(nodes.data(), d_nodes, (size_t)(n - 1) * sizeof(Node64), hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(tris.data(), d_tris, (size_t)n * sizeof(TriRec64), hipMemcpyDeviceToHost, st));
   BCHECK(hipStreamSynchronize(st));
+  if (int rc = d2h(nodes.data(), d_nodes, (size_t)(n - 1) * sizeof(Node64))) return rc;  // pinned staging
+  if (int rc = d2h(tris.data(), d_tris, (size_t)n * sizeof(TriRec64))) return rc;
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;
@@ -421,7 +421,7 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   BCHECK(alloc((void**)&d_count, (size_t)n * 4));
   BCHECK(alloc((void**)&d_cost, (size_t)n * 4));
   BCHECK(alloc((void**)&d_leaf, (size_t)n));
-  BCHECK(hipMemcpyAsync(d_rec, face_recs.data(), (size_t)n * sizeof(TriRec64), hipMemcpyHostToDevice, st));
+  if (int rc = h2d(d_rec, face_recs.data(), (size_t)n * sizeof(TriRec64))) return rc;  // pinned staging
   BCHECK(hipMemsetAsync(d_pint, 0xFF, (size_t)n * 4, st));  // the root's parent: -1
   BCHECK(hipMemsetAsync(d_cflags, 0, (size_t)n * 4, st));
   hipEvent_t e0, e1;
@@ -473,10 +473,10 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   child2.resize(2 * (size_t)(n - 1));
   box6.resize(6 * (size_t)(n - 1));
   leaf.resize((size_t)(n - 1));
-  BCHECK(hipMemcpyAsync(child2.data(), d_child, (size_t)(n - 1) * sizeof(int2), hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(box6.data(), d_nbox, (size_t)(n - 1) * sizeof(Box6), hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(leaf.data(), d_leaf, (size_t)(n - 1), hipMemcpyDeviceToHost, st));
   BCHECK(hipStreamSynchronize(st));
+  if (int rc = d2h(child2.data(), d_child, (size_t)(n - 1) * sizeof(int2))) return rc;  // pinned staging
+  if (int rc = d2h(box6.data(), d_nbox, (size_t)(n - 1) * sizeof(Box6))) return rc;
+  if (int rc = d2h(leaf.data(), d_leaf, (size_t)(n - 1))) return rc;
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;
@@ -749,29 +749,52 @@ __global__ void k_sah_split_obj(SahTask* task, int ntask, const uint32_t* stat, 
 
 // (2, SBVH) spatial bins of the flagged tasks: a reference enters the bin of its low end, exits the bin of
 // its high end, and adds the bounds of its clipped part to every bin it spans
-__global__ void k_sah_spbin(const uint32_t* rface, const Box6* rbox, const int32_t* ptask, const SahTask* task,
-                            const uint32_t* stat, const TriRec64* rec, int m, uint32_t* spbins) {
+__global__ __launch_bounds__(kSahBlock) void k_sah_spbin(const uint32_t* rface, const Box6* rbox, const int32_t* ptask,
+                                                        const SahTask* task, const uint32_t* stat, const TriRec64* rec,
+                                                        int m, uint32_t* spbins) {
+  // a block whose 256 positions belong to one flagged task (the top levels: few, huge tasks) bins in LDS
+  // first and flushes the non-empty bins, as k_sah_bin
+  __shared__ uint32_t lb[3 * kSahBins * kSpW];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const int t = ptask[i];
-  if (t < 0 || task[t].sp < 0) return;
-  Box6 box;
-  float clo[3], ext[3];
-  task_box(stat + 12 * (size_t)t, box, clo, ext);
-  const Box6 r = rbox[i];
-  uint32_t* S = spbins + (size_t)task[t].sp * 3 * kSahBins * kSpW;
-  const TriRec64 tr = rec[rface[i]];
-  for (int k = 0; k < 3; k++) {
-    if (!((box.hi[k] - box.lo[k]) / kSahBins > 0.0f)) continue;
-    const int b0 = sp_bin(box, k, r.lo[k]), b1 = sp_bin(box, k, r.hi[k]);
-    atomicAdd(&S[(k * kSahBins + b0) * kSpW + 6], 1u);
-    atomicAdd(&S[(k * kSahBins + b1) * kSpW + 7], 1u);
-    for (int bi = b0; bi <= b1; bi++) {
-      Box6 q;
-      if (b0 == b1) q = r;
-      else if (!clip_tri(tr, k, fmaxf(sp_plane(box, k, bi), r.lo[k]), fminf(sp_plane(box, k, bi + 1), r.hi[k]), r, q)) continue;
-      uint32_t* d = S + (k * kSahBins + bi) * kSpW;
-      for (int c = 0; c < 3; c++) { atomicMin(&d[c], f2o(q.lo[c])); atomicMax(&d[3 + c], f2o(q.hi[c])); }
+  const int first = blockIdx.x * blockDim.x, last = min(m - 1, first + kSahBlock - 1);
+  const int t0 = ptask[first], t1 = ptask[last];
+  const bool one_task = t0 == t1 && t0 >= 0 && task[t0].sp >= 0;  // block-uniform
+  if (one_task) {
+    for (int k = threadIdx.x; k < 3 * kSahBins * kSpW; k += kSahBlock) lb[k] = (k % kSpW) < 3 ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+  }
+  const int t = i < m ? ptask[i] : -1;
+  if (t >= 0 && task[t].sp >= 0) {
+    Box6 box;
+    float clo[3], ext[3];
+    task_box(stat + 12 * (size_t)t, box, clo, ext);
+    const Box6 r = rbox[i];
+    uint32_t* S = one_task ? lb : spbins + (size_t)task[t].sp * 3 * kSahBins * kSpW;
+    const TriRec64 tr = rec[rface[i]];
+    for (int k = 0; k < 3; k++) {
+      if (!((box.hi[k] - box.lo[k]) / kSahBins > 0.0f)) continue;
+      const int b0 = sp_bin(box, k, r.lo[k]), b1 = sp_bin(box, k, r.hi[k]);
+      atomicAdd(&S[(k * kSahBins + b0) * kSpW + 6], 1u);
+      atomicAdd(&S[(k * kSahBins + b1) * kSpW + 7], 1u);
+      for (int bi = b0; bi <= b1; bi++) {
+        Box6 q;
+        if (b0 == b1) q = r;
+        else if (!clip_tri(tr, k, fmaxf(sp_plane(box, k, bi), r.lo[k]), fminf(sp_plane(box, k, bi + 1), r.hi[k]), r, q)) continue;
+        uint32_t* d = S + (k * kSahBins + bi) * kSpW;
+        for (int c = 0; c < 3; c++) { atomicMin(&d[c], f2o(q.lo[c])); atomicMax(&d[3 + c], f2o(q.hi[c])); }
+      }
+    }
+  }
+  if (one_task) {
+    __syncthreads();
+    uint32_t* gb = spbins + (size_t)task[t0].sp * 3 * kSahBins * kSpW;
+    for (int k = threadIdx.x; k < 3 * kSahBins; k += kSahBlock) {
+      const uint32_t* d = lb + k * kSpW;
+      uint32_t* g = gb + k * kSpW;
+      if (d[0] != 0xFFFFFFFFu)
+        for (int q = 0; q < 3; q++) { atomicMin(&g[q], d[q]); atomicMax(&g[3 + q], d[3 + q]); }
+      if (d[6]) atomicAdd(&g[6], d[6]);
+      if (d[7]) atomicAdd(&g[7], d[7]);
     }
   }
 }
@@ -1064,7 +1087,7 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   BCHECK(alloc((void**)&d_sfin, (cap + 1) * 4));
   BCHECK(alloc((void**)&d_side, cap));
   BCHECK(alloc((void**)&d_cnt, 32));
-  BCHECK(hipMemcpyAsync(d_rec, face_recs.data(), N * sizeof(TriRec64), hipMemcpyHostToDevice, st));
+  if (int rc = h2d(d_rec, face_recs.data(), N * sizeof(TriRec64))) return rc;  // pinned staging
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
   BCHECK(hipEventCreate(&e1));
@@ -1168,11 +1191,11 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   nchild.resize(2 * (size_t)nodes);
   ncb.resize(12 * (size_t)nodes);
   slot_face.resize(m);
-  BCHECK(hipMemcpyAsync(nchild.data(), d_nchild, 2 * (size_t)nodes * 4, hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(ncb.data(), d_ncb, 2 * (size_t)nodes * sizeof(Box6), hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(slot_face.data(), d_rface[cur], (size_t)m * 4, hipMemcpyDeviceToHost, st));
-  BCHECK(hipMemcpyAsync(ptag.data(), d_pt[cur], (size_t)m * 4, hipMemcpyDeviceToHost, st));
   BCHECK(hipStreamSynchronize(st));
+  if (int rc = d2h(nchild.data(), d_nchild, 2 * (size_t)nodes * 4)) return rc;  // pinned staging
+  if (int rc = d2h(ncb.data(), d_ncb, 2 * (size_t)nodes * sizeof(Box6))) return rc;
+  if (int rc = d2h(slot_face.data(), d_rface[cur], (size_t)m * 4)) return rc;
+  if (int rc = d2h(ptag.data(), d_pt[cur], (size_t)m * 4)) return rc;
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;

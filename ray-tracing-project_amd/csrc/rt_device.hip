@@ -182,7 +182,7 @@ __global__ void k_debug_math(int op, int n, int in_len, int out_len, const float
 // staging buffers on their own stream (host memcpy of one chunk overlaps the DMA of the other): a plain
 // hipMemcpy from pageable memory measured ~1 GB/s for the scene upload (263 ms for the 1M soup's ~250 MB,
 // BENCH_r03 build_ms.upload).
-static int h2d(void* dst, const void* src, size_t bytes) {
+int h2d(void* dst, const void* src, size_t bytes) {
   constexpr size_t kChunk = 8u << 20;
   if (bytes < 2 * kChunk) {
     HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
@@ -217,6 +217,50 @@ static int h2d(void* dst, const void* src, size_t bytes) {
     g.used[k] = true;
   }
   HIPCHECK(hipStreamSynchronize(g.st));
+  return RT_OK;
+}
+
+// Device -> host copy into pageable memory, the same way round: DMA into one pinned 8-MiB staging buffer
+// while the host copies the other out (the device builders' read-backs).
+int d2h(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kChunk = 8u << 20;
+  if (bytes < 2 * kChunk) {
+    HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+  }
+  struct Stage {
+    void* buf[2] = {nullptr, nullptr};
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    ~Stage() {
+      if (st) (void)hipStreamSynchronize(st);
+      for (int k = 0; k < 2; k++) {
+        if (ev[k]) (void)hipEventDestroy(ev[k]);
+        if (buf[k]) (void)hipHostFree(buf[k]);
+      }
+      if (st) (void)hipStreamDestroy(st);
+    }
+  } g;
+  HIPCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+  for (int k = 0; k < 2; k++) {
+    HIPCHECK(hipHostMalloc(&g.buf[k], kChunk, hipHostMallocDefault));
+    HIPCHECK(hipEventCreateWithFlags(&g.ev[k], hipEventDisableTiming));
+  }
+  const size_t nchunks = (bytes + kChunk - 1) / kChunk;
+  auto issue = [&](size_t c) -> int {
+    const size_t off = c * kChunk, n = std::min(kChunk, bytes - off);
+    HIPCHECK(hipMemcpyAsync(g.buf[c & 1], static_cast<const char*>(src) + off, n, hipMemcpyDeviceToHost, g.st));
+    HIPCHECK(hipEventRecord(g.ev[c & 1], g.st));
+    return RT_OK;
+  };
+  int rc = issue(0);
+  if (rc) return rc;
+  for (size_t c = 0; c < nchunks; c++) {
+    if (c + 1 < nchunks && (rc = issue(c + 1))) return rc;  // the next chunk's DMA overlaps this copy-out
+    HIPCHECK(hipEventSynchronize(g.ev[c & 1]));
+    const size_t off = c * kChunk, n = std::min(kChunk, bytes - off);
+    memcpy(static_cast<char*>(dst) + off, g.buf[c & 1], n);
+  }
   return RT_OK;
 }
 

@@ -558,6 +558,7 @@ extern "C" void rt_scene_opts_default(rt_scene_opts* o) {
   o->leaf_size = 0;
   o->frames_in_flight = 4;
   o->builder = RT_BUILDER_SBVH_GPU;  // host RT_BUILDER_SBVH when there is no device
+  o->box_builder = RT_BOXES_GPU;     // host partition when there is no device (same boxes and order)
   for (int k = 0; k < 3; k++) { o->default_material.ka[k] = 0.2f; o->background[k] = 0.9f; }
   o->default_material.kd[0] = 0.9f; o->default_material.kd[1] = 0.9f; o->default_material.kd[2] = 0.0f;
   o->default_material.shininess = 0.0f;

@@ -81,6 +81,9 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
 bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, double* gpu_ms);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
+// host <-> device copies of large pageable buffers through pinned staging (rt_device.hip)
+int h2d(void* dst, const void* src, size_t bytes);
+int d2h(void* dst, const void* src, size_t bytes);
 void build_bvh4(HostScene& hs);
 void build_wide(HostScene& hs);
 float bvh_pad(const float lo[3], const float hi[3]);

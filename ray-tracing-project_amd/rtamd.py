@@ -290,7 +290,7 @@ RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 
 def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=5,
-               box_builder=0, wide_tree=0):
+               box_builder=1, wide_tree=0):
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
     o.builder = builder
@@ -308,7 +308,7 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, backgr
 
 class Scene:
     def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=5,
-                 box_builder=0, wide_tree=0, shape_model_matrix=None):
+                 box_builder=1, wide_tree=0, shape_model_matrix=None):
         """shape_model_matrix: the desc's getShapeModelMatrix() override (column-major 4x4), e.g. the oracle's
         after Mesh.set_model; default the loader's normalisation."""
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)

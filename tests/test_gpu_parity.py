@@ -546,7 +546,7 @@ def test_gpu_box_partition(rt, orc, soup, name):
     oracle's boxes (bounds bit for bit), box order and in-box face order, hence the same tie-break
     ranks; and the host builder's, too."""
     mesh, omesh, mf = _box_case(rt, orc, soup, name)
-    host = rt.Scene(mesh, min_faces=mf)
+    host = rt.Scene(mesh, min_faces=mf, box_builder=rt.RT_BOXES_HOST)
     dev = rt.Scene(mesh, min_faces=mf, box_builder=rt.RT_BOXES_GPU)
     ih, idv = host.info(), dev.info()
     assert ih["box_builder"] == rt.RT_BOXES_HOST and idv["box_builder"] == rt.RT_BOXES_GPU
