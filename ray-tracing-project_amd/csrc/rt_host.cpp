@@ -1559,19 +1559,21 @@ void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) 
     if (!is_leaf(nd.child0)) st.push_back({nd.child0, d + 1});
   }
   hs.nodes.resize(order.size());
-  for (size_t i = 0; i < order.size(); i++) {
-    Node64 nd = tmp[order[i]];
-    if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
-    if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
-    hs.nodes[i] = nd;
-  }
+  int leaves[16] = {};
+  const int T = parallel_chunks(order.size(), [&](size_t b, size_t e, int t) {
+    for (size_t i = b; i < e; i++) {
+      Node64 nd = tmp[order[i]];
+      if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
+      if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
+      leaves[t] += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
+      nd.pad0 = octant_order(nd);
+      hs.nodes[i] = nd;
+    }
+  });
   hs.root = 0;
   hs.depth = depth;
   hs.leaves = 0;
-  for (Node64& nd : hs.nodes) {
-    hs.leaves += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
-    nd.pad0 = octant_order(nd);
-  }
+  for (int t = 0; t < T; t++) hs.leaves += leaves[t];
 }
 
 // SBVH build (SbvhBuilder) from the face references; leaves get their triangle slots depth first (the
@@ -1851,18 +1853,22 @@ bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, d
   const size_t nn = nchild.size() / 2;
   const float pad = bvh_pad(lo, hi);
   std::vector<Node64> tmp(nn);
-  for (size_t k = 0; k < nn; k++) {
-    Node64 nd{};
-    for (int side = 0; side < 2; side++) {
-      const float* b = &ncb[12 * k + 6 * side];  // lo xyz, hi xyz
-      const uint32_t h = nchild[2 * k + side];
-      if (!is_leaf(h) && h >= nn) return false;
-      float* o = side ? &nd.c1lx : &nd.c0lx;  // lx hx ly hy lz hz
-      o[0] = b[0] - pad; o[1] = b[3] + pad; o[2] = b[1] - pad; o[3] = b[4] + pad; o[4] = b[2] - pad; o[5] = b[5] + pad;
-      (side ? nd.child1 : nd.child0) = h;
+  std::atomic<bool> bad{false};
+  parallel_chunks(nn, [&](size_t kb, size_t ke, int) {
+    for (size_t k = kb; k < ke; k++) {
+      Node64 nd{};
+      for (int side = 0; side < 2; side++) {
+        const float* b = &ncb[12 * k + 6 * side];  // lo xyz, hi xyz
+        const uint32_t h = nchild[2 * k + side];
+        if (!is_leaf(h) && h >= nn) bad = true;
+        float* o = side ? &nd.c1lx : &nd.c0lx;  // lx hx ly hy lz hz
+        o[0] = b[0] - pad; o[1] = b[3] + pad; o[2] = b[1] - pad; o[3] = b[4] + pad; o[4] = b[2] - pad; o[5] = b[5] + pad;
+        (side ? nd.child1 : nd.child0) = h;
+      }
+      tmp[k] = nd;
     }
-    tmp[k] = nd;
-  }
+  });
+  if (bad) return false;
   HostScene trial;
   relayout_dfs(trial, tmp, 0);
   if (trial.depth > kMaxDepth + 2) return false;  // too deep for the wave stack: host SAH instead
@@ -1870,7 +1876,9 @@ bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, d
     fprintf(stderr, "[rt] %s: %d levels, %zu nodes, %zu references, depth %d\n", spatial ? "sbvh-gpu" : "sah-gpu", levels, nn,
             slot_face.size(), trial.depth);
   std::vector<TriRec64> tris(slot_face.size());
-  for (size_t sl = 0; sl < slot_face.size(); sl++) tris[sl] = recs[slot_face[sl]];
+  parallel_chunks(slot_face.size(), [&](size_t b, size_t e, int) {
+    for (size_t sl = b; sl < e; sl++) tris[sl] = recs[slot_face[sl]];
+  });
   hs.nodes = std::move(trial.nodes);
   hs.root = 0;
   hs.depth = trial.depth;
