@@ -1215,6 +1215,11 @@ static int parallel_chunks(size_t n, F&& f) {
   return T;
 }
 
+// [0, n) in contiguous chunks on up to 16 threads (one below 64k items): f(begin, end)
+void parallel_for(size_t n, const std::function<void(size_t, size_t)>& f) {
+  parallel_chunks(n, [&](size_t b, size_t e, int) { f(b, e); });
+}
+
 // A face whose interpolated normal (interpolateNormal, flyscene.cpp:594-599) can never be the zero
 // vector for a point that passed the inside test: its area A (same expression the kernel uses) is a
 // positive normal number and every unit vertex normal leans into the face normal (n.nk >= 0.5). Then
@@ -2132,20 +2137,24 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   hs.wv.resize(hs.nv);
   hs.vnn.resize(hs.nv);
   hs.ov3.resize(3 * (size_t)hs.nv);
-  for (int32_t i = 0; i < hs.nv; i++) {
-    const float* v = d->vertices + 4 * (size_t)i;
-    memcpy(&hs.ov3[3 * (size_t)i], v, 12);
-    hs.wv[i] = rt::affv3(hs.M, f3{v[0] / v[3], v[1] / v[3], v[2] / v[3]});
-    const float* n = d->vertex_normals + 3 * (size_t)i;
-    hs.vnn[i] = rt::normalized(f3{n[0], n[1], n[2]});
-  }
+  rt::parallel_for((size_t)hs.nv, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; i++) {
+      const float* v = d->vertices + 4 * i;
+      memcpy(&hs.ov3[3 * i], v, 12);
+      hs.wv[i] = rt::affv3(hs.M, f3{v[0] / v[3], v[1] / v[3], v[2] / v[3]});
+      const float* n = d->vertex_normals + 3 * i;
+      hs.vnn[i] = rt::normalized(f3{n[0], n[1], n[2]});
+    }
+  });
   hs.fnn.resize(hs.nf);
   hs.fdist.resize(hs.nf);
-  for (int32_t f = 0; f < hs.nf; f++) {
-    const float* n = d->face_normals + 3 * (size_t)f;
-    hs.fnn[f] = rt::normalized(f3{n[0], n[1], n[2]});
-    hs.fdist[f] = rt::dot(hs.fnn[f], hs.wv[hs.fidx[3 * f]]);
-  }
+  rt::parallel_for((size_t)hs.nf, [&](size_t b, size_t e) {
+    for (size_t f = b; f < e; f++) {
+      const float* n = d->face_normals + 3 * f;
+      hs.fnn[f] = rt::normalized(f3{n[0], n[1], n[2]});
+      hs.fdist[f] = rt::dot(hs.fnn[f], hs.wv[hs.fidx[3 * f]]);
+    }
+  });
   rt::accept_region(hs);
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };

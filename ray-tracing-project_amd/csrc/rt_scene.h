@@ -1,5 +1,6 @@
 // rt_scene.h -- internal definitions of rt_mesh / rt_scene (host + device halves).
 #pragma once
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -81,6 +82,8 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
 bool build_bvh_sah_gpu(HostScene& hs, int device, int leaf_size, bool spatial, double* gpu_ms);
 int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const float lo[3], const float hi[3],
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
+// [0, n) in contiguous chunks on up to 16 host threads: f(begin, end) (rt_host.cpp)
+void parallel_for(size_t n, const std::function<void(size_t, size_t)>& f);
 // host <-> device copies of large pageable buffers through pinned staging (rt_device.hip)
 int h2d(void* dst, const void* src, size_t bytes);
 int d2h(void* dst, const void* src, size_t bytes);

@@ -719,3 +719,24 @@ def test_default_device_builder_edge_scenes(rt, case):
         assert (np.asarray(a[1]) >= 0).sum() > 1000, case
         for x, y in zip(a[:3], b[:3]):
             assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (case, m)
+
+
+def test_device_builders_large_scene(rt):
+    """The device builders at 3M triangles (3x the BASELINE scenes: reference budget, task and bin arrays
+    sized from the face count): the SBVH and binned-SAH device trees are sound by the host validator and
+    render the same frame bit for bit; the SBVH tree's SAH cost is the lower one."""
+    mesh, _, _ = rt.soup_mesh(3_000_000, 99)
+    sb = rt.Scene(mesh, builder=rt.RT_BUILDER_SBVH_GPU)
+    sa = rt.Scene(mesh, builder=rt.RT_BUILDER_SAH_GPU)
+    assert sb.info()["builder"] == rt.RT_BUILDER_SBVH_GPU and sa.info()["builder"] == rt.RT_BUILDER_SAH_GPU
+    for sc in (sb, sa):
+        v = sc.validate_bvh()
+        assert v["ok"] and v["covered2"] >= 3_000_000, v
+    assert sb.tree_cost()["sah"] < sa.tree_cost()["sah"]
+    W, H = 960, 540
+    cam = rt.flycam(W, H, 0, 0, 20)
+    a = sb.render(cam, rt.DEFAULT_LIGHTS, W, H, want_hits=True)
+    b = sa.render(cam, rt.DEFAULT_LIGHTS, W, H, want_hits=True)
+    assert (np.asarray(a[1]) >= 0).sum() > W * H // 2
+    for x, y in zip(a[:3], b[:3]):
+        assert np.asarray(x).tobytes() == np.asarray(y).tobytes()
