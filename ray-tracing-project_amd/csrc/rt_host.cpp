@@ -2161,7 +2161,7 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   s->prep_ms = ms_since(t0);
   auto t1 = clk::now();
   bool boxes_done = false;
-  if (s->opts.box_builder == RT_BOXES_GPU && s->opts.device != RT_DEVICE_NONE) {
+  if (s->opts.box_builder == RT_BOXES_GPU && s->opts.device != RT_DEVICE_NONE && hs.nf > 0) {  // (a face-less scene: host)
     int dev = s->opts.device;
     if (dev < 0) dev = rt::current_device();
     bool nonfinite = false;
