@@ -442,6 +442,8 @@ def main():
     ap.add_argument("--builder", choices=["sbvh", "sah", "lbvh", "ploc", "sahgpu", "sbvhgpu"], default="sbvhgpu",
                     help="BVH builder: SAH with spatial splits on the device (default) or the host, binned SAH on "
                          "the host or the device, or the device LBVH or PLOC (SURVEY f2)")
+    ap.add_argument("--boxes", choices=["gpu", "host"], default="gpu",
+                    help="reference box partition builder (rt_scene_opts.box_builder; identical boxes either way)")
     ap.add_argument("--wide", action="store_true",
                     help="also build the fp32 4-wide tree and walk it for PRIMARY packets (rt_scene_opts.wide_tree)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
@@ -505,7 +507,7 @@ def main():
         else:
             mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         return rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight, builder=builder,
-                        wide_tree=1 if a.wide else 0)
+                        wide_tree=1 if a.wide else 0, box_builder=0 if a.boxes == "host" else 1)
 
     # N > 1 (one node): the scene is built once -- rank 0 builds it and writes the f1 scene cache
     # (rt_scene_save), the other ranks load it (rt_scene_load: no OBJ parse, no box partition, no BVH

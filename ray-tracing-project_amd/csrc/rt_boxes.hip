@@ -297,7 +297,8 @@ int gpu_build_ref_boxes(int device, HostScene& hs, const float* v4, int32_t min_
   *nonfinite_out = false;
   XCHECK(hipSetDevice(device));
   hipStream_t st;
-  XCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  st = (hipStream_t)build_stream(device);
+  if (!st) return RT_ERR_HIP;
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
@@ -306,7 +307,6 @@ int gpu_build_ref_boxes(int device, HostScene& hs, const float* v4, int32_t min_
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
       for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-      (void)hipStreamDestroy(st);
     }
   } g{st, {}, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {

@@ -297,14 +297,14 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   if (n < 2) { set_error("gpu_build_lbvh: needs at least 2 triangles"); return RT_ERR_INVALID; }
   BCHECK(hipSetDevice(device));
   hipStream_t st;
-  BCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  st = (hipStream_t)build_stream(device);
+  if (!st) return RT_ERR_HIP;
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
     ~Guard() {
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
-      (void)hipStreamDestroy(st);
     }
   } g{st, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {
@@ -381,14 +381,14 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   radius = std::max(1, std::min(radius, kPlocMaxRadius));
   BCHECK(hipSetDevice(device));
   hipStream_t st;
-  BCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  st = (hipStream_t)build_stream(device);
+  if (!st) return RT_ERR_HIP;
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
     ~Guard() {
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
-      (void)hipStreamDestroy(st);
     }
   } g{st, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {
@@ -1043,14 +1043,14 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   if (cap < N) { set_error("gpu_build_sah: too many faces"); return RT_ERR_INVALID; }
   BCHECK(hipSetDevice(device));
   hipStream_t st;
-  BCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  st = (hipStream_t)build_stream(device);
+  if (!st) return RT_ERR_HIP;
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
     ~Guard() {
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
-      (void)hipStreamDestroy(st);
     }
   } g{st, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {

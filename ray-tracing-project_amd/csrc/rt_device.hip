@@ -3,6 +3,8 @@
 // rt_variants.hip); this file instantiates the product kernels, holds the non-template kernels (dispatch
 // order, box colours, output path, known-answer tests) and the host glue (scene upload, frame dispatch,
 // ray-list queries).
+#include <mutex>
+
 #include "rt_kernels.h"
 
 namespace rt {
@@ -182,6 +184,25 @@ __global__ void k_debug_math(int op, int n, int in_len, int out_len, const float
 // staging buffers on their own stream (host memcpy of one chunk overlaps the DMA of the other): a plain
 // hipMemcpy from pageable memory measured ~1 GB/s for the scene upload (263 ms for the 1M soup's ~250 MB,
 // BENCH_r03 build_ms.upload).
+// One stream per device for scene construction (the builders' kernels, the staged copies): created on
+// first use and kept for the process, so building scenes creates no HIP streams beyond it. Each stream a
+// process creates is bound to one of the device's few hardware queues; transient build streams created
+// before a scene's frame-slot streams changed which queues those landed on.
+void* build_stream(int device) {
+  static std::mutex mu;
+  static hipStream_t st[64] = {};
+  if (device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!st[device]) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st[device], hipStreamNonBlocking) != hipSuccess)
+      st[device] = nullptr;
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  return (void*)st[device];
+}
+
 int h2d(void* dst, const void* src, size_t bytes) {
   constexpr size_t kChunk = 8u << 20;
   if (bytes < 2 * kChunk) {
@@ -199,10 +220,12 @@ int h2d(void* dst, const void* src, size_t bytes) {
         if (ev[k]) (void)hipEventDestroy(ev[k]);
         if (buf[k]) (void)hipHostFree(buf[k]);
       }
-      if (st) (void)hipStreamDestroy(st);
     }
   } g;
-  HIPCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  g.st = (hipStream_t)build_stream(dev);
+  if (!g.st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
   for (int k = 0; k < 2; k++) {
     HIPCHECK(hipHostMalloc(&g.buf[k], kChunk, hipHostMallocDefault));
     HIPCHECK(hipEventCreateWithFlags(&g.ev[k], hipEventDisableTiming));
@@ -238,10 +261,12 @@ int d2h(void* dst, const void* src, size_t bytes) {
         if (ev[k]) (void)hipEventDestroy(ev[k]);
         if (buf[k]) (void)hipHostFree(buf[k]);
       }
-      if (st) (void)hipStreamDestroy(st);
     }
   } g;
-  HIPCHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  g.st = (hipStream_t)build_stream(dev);
+  if (!g.st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
   for (int k = 0; k < 2; k++) {
     HIPCHECK(hipHostMalloc(&g.buf[k], kChunk, hipHostMallocDefault));
     HIPCHECK(hipEventCreateWithFlags(&g.ev[k], hipEventDisableTiming));

@@ -84,6 +84,8 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
                    int leaf_size, float pad, std::vector<Node64>& nodes, std::vector<TriRec64>& tris, double* gpu_ms);
 // [0, n) in contiguous chunks on up to 16 host threads: f(begin, end) (rt_host.cpp)
 void parallel_for(size_t n, const std::function<void(size_t, size_t)>& f);
+// the device's scene-construction stream (rt_device.hip; created once, never destroyed)
+void* build_stream(int device);  // a hipStream_t
 // host <-> device copies of large pageable buffers through pinned staging (rt_device.hip)
 int h2d(void* dst, const void* src, size_t bytes);
 int d2h(void* dst, const void* src, size_t bytes);
