@@ -22,6 +22,12 @@ for s in $STEPS; do
     ploc)
       timeout -k 10 300 python bench.py --steps 20 --warmup 5 --builder ploc --no-cpu --no-side > $OUT/bench_ploc.json 2> $OUT/bench_ploc.err
       rc=$?; echo "ploc rc=$rc"; cat $OUT/bench_ploc.json; hard $rc ;;
+    profc2)
+      OUTDIR=$OUT/profc2 \
+      BENCH_ARGS="--scene bunny --mode primary --steps 20 --warmup 3 --no-cpu --no-extra --no-e2e --no-side --frames-in-flight 1" \
+      PMC_ARGS="--scene bunny --mode primary --steps 5 --warmup 1 --no-cpu --no-stats --no-extra --no-e2e --no-side --frames-in-flight 1" \
+      bash tools/profile.sh > $OUT/profile_c2.log 2>&1
+      rc=$?; echo "profile c2 rc=$rc"; tail -12 $OUT/profile_c2.log; hard $rc ;;
     plocsweep)
       # PLOC A/B: neighbour radius x collapse node cost x leaf rule (C3, --builder ploc), then the SBVH line
       export RTAMD_DEBUG_KNOBS=1
