@@ -263,10 +263,20 @@ def shared_scene(build, load, rank, barrier, path):
     return sc, setup_s
 
 
-def kernel_bound(kernel):
-    """The limiter of `kernel` in the newest committed rocprofv3 summary (profiles/*_pmc.json, by file
-    time of the tag order): "latency", "hbm", "valu" or "salu" from its `limiter` text."""
+def kernel_bound(kernel, latest=None):
+    """The limiter of `kernel`: from the workload's own committed profile (profiles/<latest>, e.g.
+    pmc_latest_c2.json for the C2 sub-line) when that profile is of this kernel, else from the newest
+    committed rocprofv3 summary of the kernel (profiles/*_pmc.json, by tag order): "latency", "hbm", "valu"
+    or "salu" from its `limiter` text."""
     import glob
+    if latest:
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", latest)))
+            if str(d.get("kernel", "")).startswith(kernel + "<") and d.get("limiter"):
+                lim = str(d["limiter"]).split(":")[0].strip().lower()
+                return lim, f"profiles/{d.get('tag')}_pmc.json: {d['limiter']}"
+        except (OSError, ValueError):
+            pass
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
         try:
@@ -342,7 +352,7 @@ def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash
         limiter = prof.get("limiter")
     # what bounds the kernel, as the newest committed profile of it measured: the
     # roofline below is still priced against HBM bandwidth, the resource north_star names
-    bound, bound_src = kernel_bound(kname)
+    bound, bound_src = kernel_bound(kname, latest)
     roof = {"bound": bound, "bound_source": bound_src, "priced_against": "hbm",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
