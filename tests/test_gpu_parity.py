@@ -740,3 +740,28 @@ def test_device_builders_large_scene(rt):
     assert (np.asarray(a[1]) >= 0).sum() > W * H // 2
     for x, y in zip(a[:3], b[:3]):
         assert np.asarray(x).tobytes() == np.asarray(y).tobytes()
+
+
+@pytest.mark.parametrize("builder", ["sbvh", "sbvhgpu", "sahgpu"])
+@pytest.mark.parametrize("leaf", [1, 2, 8, 16])
+def test_leaf_sizes_render_identical_bits(rt, soup, builder, leaf):
+    """Leaf bounds 1..kMaxLeaf (16) through the host and device builders: the leaf loops (and the leaf-entry
+    prefetch of a leaf's remaining triangle records) give the frame of the default scene bit for bit, PRIMARY
+    and FULL, binary and 4-wide trees; the bunny and the 1M soup."""
+    bid = {"sbvh": rt.RT_BUILDER_SBVH, "sbvhgpu": rt.RT_BUILDER_SBVH_GPU, "sahgpu": rt.RT_BUILDER_SAH_GPU}[builder]
+    bunny = rt.Mesh.load_obj(scene_path("bunny.obj"))
+    ref_b = rt.Scene(bunny)
+    ref_s, _ = soup
+    cases = [(bunny, ref_b, (960, 540))]
+    if builder != "sbvh" or leaf == 16:  # the 1M soup's host SBVH takes seconds per build: its largest leaves only
+        cases.append((ref_s.mesh, ref_s, (640, 360)))
+    for mesh, ref, (W, H) in cases:
+        sc = rt.Scene(mesh, builder=bid, leaf_size=leaf, wide_tree=1 if leaf >= 8 else 0)
+        v = sc.validate_bvh()
+        assert v["ok"], v
+        cam = rt.flycam(W, H, 0, 0, 20)
+        for m in (rt.RT_MODE_PRIMARY, rt.RT_MODE_FULL):
+            a = ref.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+            b = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+            for x, y in zip(a[:3], b[:3]):
+                assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), (builder, leaf, m)
