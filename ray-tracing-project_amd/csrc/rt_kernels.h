@@ -191,12 +191,9 @@ __device__ __forceinline__ Span slab(float lx, float hx, float ly, float hy, flo
 // The same span when the wave's active rays share one direction octant (OCT bit k: axis k negative,
 // by the sign of the nudged reciprocal): fma(., id, offset) is monotone in the box coordinate, so the
 // near / far plane of each axis is known and min(t0, t1) / max(t0, t1) are exactly the near / far
-// values -- identical results with 8 fewer min/max per child. OCT < 0: the generic test.
-// CLIP = false (octant loops of packets whose rays all start in front of the scene, trace_oct): the entry
-// distance is not clipped at 0. That admits a superset of boxes (max(tmin, 0) >= tmin), so culling stays
-// conservative, and for such a packet it admits no extra box: every box lies inside the root's, which
-// each ray enters at t >= 0 or misses, and the rounded plane distances are monotone in the coordinates.
-template <int OCT, bool CLIP = true>
+// values -- identical results with 8 fewer min/max per child. OCT < 0: the generic test. (An unclipped
+// entry distance for packets starting in front of the scene measured within noise, r03_micro_ab.txt.)
+template <int OCT>
 __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, float lz, float hz, const Ray& r,
                                        float tmax_ray) {
   if (OCT < 0) return slab(lx, hx, ly, hy, lz, hz, r, tmax_ray);
@@ -208,12 +205,8 @@ __device__ __forceinline__ Span slab_o(float lx, float hx, float ly, float hy, f
   const float noy = (OCT & 2) ? r.ob.y : r.oa.y, foy = (OCT & 2) ? r.oa.y : r.ob.y;
   const float noz = (OCT & 4) ? r.ob.z : r.oa.z, foz = (OCT & 4) ? r.oa.z : r.ob.z;
   Span s;
-  if (CLIP)
-    s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
-                   fmaxf(__builtin_fmaf(nz, r.id.z, noz), 0.0f));
-  else
-    s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
-                   __builtin_fmaf(nz, r.id.z, noz));
+  s.tmin = fmaxf(fmaxf(__builtin_fmaf(nx, r.id.x, nox), __builtin_fmaf(ny, r.id.y, noy)),
+                 fmaxf(__builtin_fmaf(nz, r.id.z, noz), 0.0f));
   // min of the three far planes and tmax_ray in two instructions (the compiler's fminf would first
   // canonicalise tmax_ray, a loop-carried value, with an extra v_max per node)
   asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
@@ -513,7 +506,7 @@ __device__ __forceinline__ void lds_push(uint32_t* slot, uint32_t v) {
 // by the node's order bit for this octant) is pushed at once; both slab tests give the lane masks; an
 // 8-SALU block picks the next node (near child, the one child needed, or the pop marker) and keeps the
 // push only when both children are needed.
-template <bool ANY, int OCT, bool CLIP = true>
+template <bool ANY, int OCT>
 __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                                    uint32_t* lds_stack, uint32_t node, int sp) {
   // lanes still tracing: used by the any-hit triangle tests only (a closest-hit lane without a ray
@@ -544,8 +537,8 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
       const float tcut = ANY ? tlim : h.t;
       Ray rb = r;
       rb.id = rid;
-      const Span s0 = slab_o<OCT, CLIP>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, rb, tcut);
-      const Span s1 = slab_o<OCT, CLIP>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, rb, tcut);
+      const Span s0 = slab_o<OCT>(nd.c0lx, nd.c0hx, nd.c0ly, nd.c0hy, nd.c0lz, nd.c0hz, rb, tcut);
+      const Span s1 = slab_o<OCT>(nd.c1lx, nd.c1hx, nd.c1ly, nd.c1hy, nd.c1lz, nd.c1hz, rb, tcut);
       const uint64_t m0 = mask_le(s0.tmin, s0.tmax), m1 = mask_le(s1.tmin, s1.tmax);
       uint32_t nxt, far, ta, tb;
       uint64_t tt;
@@ -627,11 +620,11 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
   if (!ANY && !active) h.t = INFINITY;
 }
 
-template <bool ANY, int OCT, bool CLIP = true>
+template <bool ANY, int OCT>
 __device__ __forceinline__ void traverse_fast(const DevScene& P, const Ray& r, bool active, Hit& h, bool& found,
                                               uint32_t* lds_stack) {
   if (P.n_nodes == 0) return;
-  traverse_fast_from<ANY, OCT, CLIP>(P, r, active, h, found, lds_stack, P.root, 0);
+  traverse_fast_from<ANY, OCT>(P, r, active, h, found, lds_stack, P.root, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
