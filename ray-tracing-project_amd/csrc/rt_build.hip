@@ -1042,6 +1042,7 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   const size_t cap = std::min<size_t>(spatial ? N + (size_t)(budget * (double)N) + 1 : N, (size_t)kMaxFaces);
   if (cap < N) { set_error("gpu_build_sah: too many faces"); return RT_ERR_INVALID; }
   BCHECK(hipSetDevice(device));
+  PhaseTimer pt("gpu_build_sah");
   hipStream_t st;
   st = (hipStream_t)build_stream(device);
   if (!st) return RT_ERR_HIP;
@@ -1087,7 +1088,9 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   BCHECK(alloc((void**)&d_sfin, (cap + 1) * 4));
   BCHECK(alloc((void**)&d_side, cap));
   BCHECK(alloc((void**)&d_cnt, 32));
+  pt.mark("alloc");
   if (int rc = h2d(d_rec, face_recs.data(), N * sizeof(TriRec64))) return rc;  // pinned staging
+  pt.mark("h2d_records");
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
   BCHECK(hipEventCreate(&e1));
@@ -1192,10 +1195,12 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   ncb.resize(12 * (size_t)nodes);
   slot_face.resize(m);
   BCHECK(hipStreamSynchronize(st));
+  pt.mark("levels");
   if (int rc = d2h(nchild.data(), d_nchild, 2 * (size_t)nodes * 4)) return rc;  // pinned staging
   if (int rc = d2h(ncb.data(), d_ncb, 2 * (size_t)nodes * sizeof(Box6))) return rc;
   if (int rc = d2h(slot_face.data(), d_rface[cur], (size_t)m * 4)) return rc;
   if (int rc = d2h(ptag.data(), d_pt[cur], (size_t)m * 4)) return rc;
+  pt.mark("d2h");
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;

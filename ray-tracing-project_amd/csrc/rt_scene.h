@@ -1,5 +1,7 @@
 // rt_scene.h -- internal definitions of rt_mesh / rt_scene (host + device halves).
 #pragma once
+#include <chrono>
+#include <cstdio>
 #include <functional>
 #include <string>
 #include <vector>
@@ -86,6 +88,8 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
 void parallel_for(size_t n, const std::function<void(size_t, size_t)>& f);
 // the device's scene-construction stream (rt_device.hip; created once, never destroyed)
 void* build_stream(int device);  // a hipStream_t
+// first-use initialisation of the device (its build stream, a first allocation); thread-safe (rt_device.hip)
+void device_warmup(int device);
 // host <-> device copies of large pageable buffers through pinned staging (rt_device.hip)
 int h2d(void* dst, const void* src, size_t bytes);
 int d2h(void* dst, const void* src, size_t bytes);
@@ -107,6 +111,19 @@ void set_error(const char* fmt, ...);
 // else nullptr -- the product library's behaviour never depends on the caller's environment otherwise.
 const char* debug_env(const char* name);
 void set_debug_env(bool on);
+// RT_TIMING phase log (debug knobs only): mark(name) prints the ms since the previous mark (or construction)
+struct PhaseTimer {
+  const char* scope;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseTimer(const char* sc) : scope(sc), on(debug_env("RT_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* name) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[rt] %s/%s %.1f ms\n", scope, name, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
 
 }  // namespace rt
 
