@@ -208,10 +208,14 @@ void* build_stream(int device) {
 // while rt_scene_create prepares the host arrays: measured ~0.14 s before the first builder's allocations
 // on a fresh process (C3, RT_TIMING), which otherwise adds to the scene setup after the host preparation.
 void device_warmup(int device) {
+  PhaseTimer pt("warmup");
   if (device < 0 || hipSetDevice(device) != hipSuccess) return;
+  pt.mark("set_device");
   (void)build_stream(device);
+  pt.mark("stream");
   void* p = nullptr;
   if (hipMalloc(&p, 1u << 20) == hipSuccess) (void)hipFree(p);
+  pt.mark("malloc");
 }
 
 int h2d(void* dst, const void* src, size_t bytes) {
@@ -342,6 +346,7 @@ int device_upload(rt_scene* s) {
   int rc;
   s->static_pad = scene_static_pad(hs);
   s->cert_origin_max = cert_origin_max(hs);
+  pt.mark("pads");
   {
     // BVH nodes and triangle records share one allocation (triangles right after the nodes), so one
     // base plus a 32-bit byte offset reaches either: each uploaded node's pad0 / pad1
@@ -361,6 +366,7 @@ int device_upload(rt_scene* s) {
     s->wide_base = (uint32_t)wide_base;
     s->wide_copy_bytes = wide_base ? (uint32_t)(nw * sizeof(Node128)) : 0;
     if ((rc = dalloc_copy(&s->d_nodes, nullptr, bytes, tot))) return rc;
+    pt.mark("alloc");
     // the device form of the binary records, filled on the host threads (no value-initialisation pass):
     // pad0 / pad1 = the children's record offsets (prefetch targets) with the octant order bits in their
     // low bits, interior children as byte offsets of their records (node_offset)
@@ -381,7 +387,7 @@ int device_upload(rt_scene* s) {
         }
       });
     }
-    pt.mark("alloc+node_prep");
+    pt.mark("node_prep");
     if (nn && (rc = h2d(s->d_nodes, nodes.get(), nn * 64))) return rc;
     pt.mark("h2d_nodes");
     s->d_tris = reinterpret_cast<TriRec64*>(s->d_nodes + nn);

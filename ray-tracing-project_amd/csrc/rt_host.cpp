@@ -803,7 +803,10 @@ struct BvhBuilder {
     {
       Aabb pb[16], pc[16];
       const int T = chunked(b, e, [&](uint32_t lo, uint32_t hi, int t) {
-        for (uint32_t i = lo; i < hi; i++) { pb[t].grow(prims[i].lo, prims[i].hi); pc[t].growp(prims[i].c); }
+        Aabb a, c;  // thread-local, stored once (no false sharing on pb / pc)
+        for (uint32_t i = lo; i < hi; i++) { a.grow(prims[i].lo, prims[i].hi); c.growp(prims[i].c); }
+        pb[t] = a;
+        pc[t] = c;
       });
       box = Aabb();
       for (int t = 0; t < T; t++) { box.merge(pb[t]); cb.merge(pc[t]); }
@@ -1044,7 +1047,10 @@ struct SbvhBuilder {
     {
       Aabb pb[16], pc[16];
       const int T = chunked(n, [&](uint32_t b, uint32_t e, int t) {
-        for (uint32_t i = b; i < e; i++) { pb[t].grow(r[i].lo, r[i].hi); pc[t].growp(r[i].c); }
+        Aabb a, c;  // thread-local, stored once
+        for (uint32_t i = b; i < e; i++) { a.grow(r[i].lo, r[i].hi); c.growp(r[i].c); }
+        pb[t] = a;
+        pc[t] = c;
       });
       for (int t = 0; t < T; t++) { box.merge(pb[t]); cb.merge(pc[t]); }
     }
@@ -1137,7 +1143,9 @@ struct SbvhBuilder {
       // reference count, hence on the leaf and node storage); without room it is an object split
       std::vector<int64_t> cnt((size_t)TB, 0);
       const int T = chunked(n, [&](uint32_t b, uint32_t e, int t) {
-        for (uint32_t i = b; i < e; i++) cnt[t] += r[i].lo[s_axis] < s_pos && r[i].hi[s_axis] > s_pos;
+        int64_t k = 0;  // thread-local
+        for (uint32_t i = b; i < e; i++) k += r[i].lo[s_axis] < s_pos && r[i].hi[s_axis] > s_pos;
+        cnt[t] = k;
       });
       int64_t straddle = 0;
       for (int t = 0; t < T; t++) straddle += cnt[t];
@@ -1256,13 +1264,23 @@ float bvh_pad(const float lo[3], const float hi[3]) {
 
 // the static pad the builders gave every box: bvh_pad of the triangles' bounds (the builders' `world`)
 float scene_static_pad(const HostScene& hs) {
+  // per-chunk bounds merged afterwards: min / max skip NaN coordinates the same way in any order
+  float plo[16][3], phi[16][3];
+  for (int t = 0; t < 16; t++)
+    for (int k = 0; k < 3; k++) { plo[t][k] = INFINITY; phi[t][k] = -INFINITY; }
+  const int T = parallel_chunks(hs.tris.size(), [&](size_t b, size_t e, int t) {
+    float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};  // thread-local (no false sharing)
+    for (size_t i = b; i < e; i++)
+      for (int j = 0; j < 3; j++) {
+        const f3& w = bound_vert(hs, hs.tris[i].face, j);
+        const float v[3] = {w.x, w.y, w.z};
+        for (int k = 0; k < 3; k++) { l[k] = std::min(l[k], v[k]); h[k] = std::max(h[k], v[k]); }
+      }
+    for (int k = 0; k < 3; k++) { plo[t][k] = l[k]; phi[t][k] = h[k]; }
+  });
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (const TriRec64& t : hs.tris)
-    for (int j = 0; j < 3; j++) {
-      const f3& w = bound_vert(hs, t.face, j);
-      const float v[3] = {w.x, w.y, w.z};
-      for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], v[k]); hi[k] = std::max(hi[k], v[k]); }
-    }
+  for (int t = 0; t < T; t++)
+    for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], plo[t][k]); hi[k] = std::max(hi[k], phi[t][k]); }
   return hs.tris.empty() ? 0.0f : bvh_pad(lo, hi);
 }
 
@@ -1270,10 +1288,12 @@ void world_bounds(const HostScene& hs, float lo[3], float hi[3]) {
   Aabb parts[16];
   const std::vector<f3>& pts = hs.av.empty() ? hs.wv : hs.av;
   const int T = parallel_chunks(pts.size(), [&](size_t b, size_t e, int t) {
+    Aabb a;  // thread-local, stored once (adjacent per-thread slots written per item share cache lines)
     for (size_t i = b; i < e; i++) {
       const float c[3] = {pts[i].x, pts[i].y, pts[i].z};
-      parts[t].growp(c);
+      a.growp(c);
     }
+    parts[t] = a;
   });
   Aabb w;
   for (int t = 0; t < T; t++) w.merge(parts[t]);
@@ -1616,14 +1636,16 @@ void relayout_dfs(HostScene& hs, const std::vector<Node64>& tmp, uint32_t root) 
   hs.nodes.resize(order.size());
   int leaves[16] = {};
   const int T = parallel_chunks(order.size(), [&](size_t b, size_t e, int t) {
+    int lv = 0;  // thread-local count (no false sharing on leaves[])
     for (size_t i = b; i < e; i++) {
       Node64 nd = tmp[order[i]];
       if (!is_leaf(nd.child0)) nd.child0 = remap[nd.child0];
       if (!is_leaf(nd.child1)) nd.child1 = remap[nd.child1];
-      leaves[t] += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
+      lv += (int)is_leaf(nd.child0) + (int)is_leaf(nd.child1);
       nd.pad0 = octant_order(nd);
       hs.nodes[i] = nd;
     }
+    leaves[t] = lv;
   });
   hs.root = 0;
   hs.depth = depth;
@@ -1705,6 +1727,7 @@ void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
   std::vector<Prim> prims(hs.nf);
   Aabb wparts[16];
   const int TW = parallel_chunks((size_t)hs.nf, [&](size_t b, size_t e, int t) {
+    Aabb wa;  // thread-local, stored once
     for (size_t f = b; f < e; f++) {
       Prim& p = prims[f];
       p.id = (uint32_t)f;
@@ -1715,8 +1738,9 @@ void build_bvh(HostScene& hs, int leaf_size, bool spatial) {
         for (int k = 0; k < 3; k++) { p.lo[k] = std::min(p.lo[k], c[k]); p.hi[k] = std::max(p.hi[k], c[k]); }
       }
       for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.lo[k] + p.hi[k]);
-      wparts[t].grow(p.lo, p.hi);
+      wa.grow(p.lo, p.hi);
     }
+    wparts[t] = wa;
   });
   Aabb world;
   for (int t = 0; t < TW; t++) world.merge(wparts[t]);
