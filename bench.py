@@ -34,6 +34,13 @@ import subprocess
 import sys
 import time
 
+# Hardware queues per process for the HIP runtime (read once at its initialisation, so set before anything
+# touches the GPU; an explicit setting in the environment wins). With the default 4, the scene's construction
+# stream and its 4 frame-slot streams share queues and the overlap of frames in flight depends on stream
+# creation order; with 8 every stream has its own queue: C3 +1.4..+3.9% at 4 frames in flight and 3 frames no
+# longer 9% down (profiles/ab/r04_hw_queues_ab.txt).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -632,7 +639,7 @@ def main():
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
                        "parallelism": (f"tiles/{n} (64x64-pixel super-tiles interleaved over ranks, scene replicated)"
                                        if n > 1 else "tiles/1 (one GPU, whole frame)"),
-                       "frames_in_flight": info_fif,
+                       "frames_in_flight": info_fif, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
                        # per-frame latency with frames in flight (first kernel start to last kernel end of one
                        # frame; frames overlap, so ms_per_step is the throughput interval) and alone
                        "kernel_ms_per_frame": round(kernel_ms_max, 4),
