@@ -38,7 +38,8 @@ import time
 # touches the GPU; an explicit setting in the environment wins). With the default 4, the scene's construction
 # stream and its 4 frame-slot streams share queues and the overlap of frames in flight depends on stream
 # creation order; with 8 every stream has its own queue: C3 +1.4..+3.9% at 4 frames in flight and 3 frames no
-# longer 9% down (profiles/ab/r04_hw_queues_ab.txt).
+# longer 9% down (profiles/ab/r04_hw_queues_ab.txt). An environment that sets it (the GPU boxes export 4) keeps
+# its value; config.hw_queues reports the one in effect.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np
