@@ -34,14 +34,6 @@ import subprocess
 import sys
 import time
 
-# Hardware queues per process for the HIP runtime (read once at its initialisation, so set before anything
-# touches the GPU; an explicit setting in the environment wins). With the default 4, the scene's construction
-# stream and its 4 frame-slot streams share queues and the overlap of frames in flight depends on stream
-# creation order; with 8 every stream has its own queue: C3 +1.4..+3.9% at 4 frames in flight and 3 frames no
-# longer 9% down (profiles/ab/r04_hw_queues_ab.txt). An environment that sets it (the GPU boxes export 4) keeps
-# its value; config.hw_queues reports the one in effect.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -183,7 +175,7 @@ def e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist, iters=5):
         t = time.perf_counter()
         sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=(rank, n))
         sc.synchronize()
-        if n == 1:
+        if n == 1 or dist is None:  # (an in-process multi-device scene assembles its frame on the host)
             host, _ = sc.download_rgb8(W, H)
         else:
             sc.pack_shard_rgb8(slc.data_ptr())
@@ -414,7 +406,8 @@ def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_de
     t0 = time.perf_counter()
     for _ in range(steps):
         sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
-    st = sc.synchronize()
+    st, per = sc.synchronize_devices()
+    st["per_device"] = per
     sync_device()
     barrier()
     el = time.perf_counter() - t0
@@ -469,6 +462,9 @@ def main():
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="one GPU renders only shard 0 of K (the per-GPU work of a K-GPU C4 run, no collective): "
                          "rehearsal of strong scaling; the line reports that shard's rate")
+    ap.add_argument("--devices", default=None,
+                    help="in-process multi-device run (no launcher): the HIP devices of the scene, e.g. 0,1,2,3 "
+                         "(default 0..N-1 for --gpus N); repeats allowed to rehearse on one GPU (0,0)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -478,9 +474,25 @@ def main():
     # BENCH_BACKEND=gloo for the timing reductions); unset in real runs (one GPU per rank)
     if "BENCH_DEVICE" in os.environ:
         local = int(os.environ["BENCH_DEVICE"])
-    if world != a.gpus and world > 1:
-        print(f"warning: WORLD_SIZE {world} != --gpus {a.gpus}", file=sys.stderr)
-    n = max(world, 1)
+    if world > 1 and world != a.gpus:
+        print(f"error: WORLD_SIZE {world} != --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+    # --gpus N without a launcher: the drop-in's own multi-device path -- one process renders every frame on
+    # N devices (rt_scene_opts.n_devices / devices: the scene replicated by peer copy, the frame's super-tiles
+    # interleaved over the devices, the tiles assembled on the host). It never falls back
+    # to fewer GPUs: too few visible devices is an error, not an n_gpus 1 line.
+    devices = None
+    if world == 1 and (a.gpus > 1 or a.devices):
+        devices = [int(x) for x in a.devices.split(",")] if a.devices else list(range(a.gpus))
+        if len(devices) != a.gpus:
+            print(f"error: --devices lists {len(devices)} devices, --gpus {a.gpus}", file=sys.stderr)
+            sys.exit(2)
+        import torch
+        visible = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        if max(devices) >= visible or min(devices) < 0:
+            print(f"error: --gpus {a.gpus} needs devices {devices}, {visible} visible", file=sys.stderr)
+            sys.exit(2)
+    n = max(world, 1) if devices is None else len(devices)
 
     import torch
     dist = None
@@ -525,7 +537,7 @@ def main():
         else:
             mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         return rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=a.frames_in_flight, builder=builder,
-                        wide_tree=1 if a.wide else 0, box_builder=0 if a.boxes == "host" else 1)
+                        wide_tree=1 if a.wide else 0, box_builder=0 if a.boxes == "host" else 1, devices=devices)
 
     # N > 1 (one node): the scene is built once -- rank 0 builds it and writes the f1 scene cache
     # (rt_scene_save), the other ranks load it (rt_scene_load: no OBJ parse, no box partition, no BVH
@@ -545,7 +557,8 @@ def main():
     setup_per_rank = gather_all(dist, dev, setup_s)
     cam = rt.flycam(W, H, 0, 0, 20)
     mode = rt.RT_MODE_FULL if a.mode == "full" else rt.RT_MODE_PRIMARY
-    shard = (0, K) if K else (rank, n)
+    # the library splits a multi-device scene's frame itself: the caller renders the whole frame
+    shard = (0, K) if K else ((0, 1) if devices else (rank, n))
 
     elapsed, st = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device)
     my_rays = st["primary_rays"] * a.steps
@@ -554,6 +567,16 @@ def main():
     kernel_ms_avg = st["kernel_ms"] / max(st["launches"], 1)
     kernel_ms_max = reduce(kernel_ms_avg, "MAX")
     ms_per_step = elapsed_max / a.steps * 1e3
+    # per GPU (rank, or device of an in-process multi-device scene): kernel ms per frame and rays per frame,
+    # so an N > 1 line shows its load balance
+    if devices:
+        per_gpu = [{"device": d, "kernel_ms_per_frame": round(p["kernel_ms"] / max(p["launches"], 1), 4),
+                    "rays_per_frame": p["primary_rays"]} for d, p in zip(devices, st["per_device"])]
+    else:
+        ks = gather_all(dist, dev, kernel_ms_avg)
+        rs = gather_all(dist, dev, float(st["primary_rays"]))
+        per_gpu = [{"rank": i, "kernel_ms_per_frame": round(k, 4), "rays_per_frame": int(r)}
+                   for i, (k, r) in enumerate(zip(ks, rs))]
 
     # the dominant kernel's launch duration with one frame on the GPU (roofline denominator)
     iso_ms, iso_trace_ms = isolated_kernel_ms(rt, sc, cam, W, H, mode, shard)
@@ -592,6 +615,9 @@ def main():
     headline_parity = None
     if rank == 0 and n == 1 and not K and a.frame is None and a.scene == "soup" and a.tris == 1_000_000:
         headline_parity = frame_parity(rt, sc, W, H, mode, "C3" if a.mode == "primary" else "C3-full")
+    elif devices and not K and a.frame is None and a.scene == "soup" and a.tris == 1_000_000 and a.mode == "primary":
+        # the in-process multi-device C4 frame, assembled from every device's tiles, against the oracle's digests
+        headline_parity = frame_parity(rt, sc, W, H, mode, "C4")
 
     gpu_frame = None
     if rank == 0 and n == 1 and not a.no_cpu:
@@ -638,9 +664,17 @@ def main():
                                    + (f", split over {n} GPUs" if n > 1 else "")
                                    + (f", REHEARSAL: shard 0 of {K} on one GPU (value = that shard's rate)" if K else ""),
                        "frame": f"{W}x{H}", "triangles": info["n_faces"], "mode": a.mode,
-                       "parallelism": (f"tiles/{n} (64x64-pixel super-tiles interleaved over ranks, scene replicated)"
+                       "parallelism": (f"tiles/{n} in one process over devices {devices} (rt_scene_opts.devices: "
+                                       "scene replicated by peer copy, 64x64-pixel super-tiles interleaved over "
+                                       "the devices, tiles assembled on the host)" if devices else
+                                       f"tiles/{n} (64x64-pixel super-tiles interleaved over ranks, scene replicated)"
                                        if n > 1 else "tiles/1 (one GPU, whole frame)"),
-                       "frames_in_flight": info_fif, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
+                       "launcher": "in-process devices" if devices else ("torchrun" if world > 1 else "none"),
+                       "per_gpu": per_gpu if n > 1 else None,
+                       "frames_in_flight": info_fif,
+                       # HIP hardware queues per process: the environment's GPU_MAX_HW_QUEUES (0 = unset, the
+                       # runtime's default 4); bench.py leaves it alone
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
                        # per-frame latency with frames in flight (first kernel start to last kernel end of one
                        # frame; frames overlap, so ms_per_step is the throughput interval) and alone
                        "kernel_ms_per_frame": round(kernel_ms_max, 4),
@@ -652,6 +686,7 @@ def main():
                        "ref_boxes": info["n_ref_boxes"], "scene_setup_s": round(setup_s, 2),
                        "scene_setup_s_per_rank": [round(x, 2) for x in setup_per_rank],
                        "scene_shared_build": cache_path is not None,
+                       "scene_replicate_ms": round(info["replicate_ms"], 1) if info["n_devices"] > 1 else None,
                        "builder": {0: "sah-host", 1: "lbvh-gpu", 2: "sbvh-host", 3: "ploc-gpu", 4: "sah-gpu", 5: "sbvh-gpu"}.get(info["builder"], str(info["builder"])),
                        "build_ms": {"prep": round(info["prep_ms"], 1), "ref_boxes": round(info["boxes_ms"], 1),
                                     "bvh": round(info["bvh_ms"], 1), "bvh_gpu_kernels": round(info["bvh_gpu_ms"], 2),

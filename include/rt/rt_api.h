@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 3  /* 3: rt_stats.wave_node_bytes, RT_BUILDER_SBVH */
+#define RT_API_VERSION 4  /* 4: multi-device scenes (rt_scene_opts.n_devices/devices, rt_synchronize_devices);
+                             3: rt_stats.wave_node_bytes, RT_BUILDER_SBVH */
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -128,7 +129,23 @@ typedef struct rt_scene_opts {
                              * rays share a direction octant. 0 (default): the binary tree only -- measured
                              * equal speed at a quarter of the memory. Results are
                              * identical either way (API 3) */
+  /* Multi-device rendering in one process (API 4; SURVEY 8(b) b2 / 8(e) e1 -- the reference's frame
+   * driver is one process, flyscene.cpp:266-289): n_devices > 1 renders every frame on the listed HIP
+   * devices together. The scene is built once (on devices[0]) and replicated to every other listed
+   * device by peer copy over xGMI; each frame's 16x16 tiles are split into 64x64-pixel super-tiles
+   * interleaved over the devices (the rt_frame shard layout: device k of D renders shard
+   * shard_index + shard_count * k of shard_count * D), each device renders on its own streams, and the
+   * frame is assembled in the caller's buffer from each device's tiles (packed on the device, copied
+   * through pinned host memory by a host worker per device): no collective. Entries may repeat (two
+   * replicas sharing one GPU). n_devices 0 (default) or 1: one device, `device` (n_devices 1: devices[0]);
+   * RT_DEVICES_ALL: every visible device. Results are bit-identical to a one-device render. Ray-list
+   * queries (rt_trace_*), diagnostics and rt_frame_pack_shard_rgb8 use devices[0] only. */
+  int32_t n_devices;
+  int32_t devices[16];      /* RT_MAX_DEVICES */
 } rt_scene_opts;
+
+#define RT_MAX_DEVICES 16
+#define RT_DEVICES_ALL (-1)
 
 #define RT_BUILDER_SAH 0
 #define RT_BUILDER_LBVH_GPU 1
@@ -165,6 +182,9 @@ typedef struct rt_scene_info {
   double boxes_gpu_ms;    /* device time of the GPU box partition (RT_BOXES_GPU) */
   int32_t wide_nodes;     /* fp32 4-wide nodes per octant copy (0: no wide tree) (API 3) */
   int32_t wide_depth;     /* its depth */
+  int32_t n_devices;      /* devices rendering the scene's frames (API 4; 1 for a single-device scene,
+                             0 host-only); device_bytes sums over them */
+  double replicate_ms;    /* time to replicate the device data to devices[1..] (0: one device) */
 } rt_scene_info;
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* out);
@@ -287,6 +307,12 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t
 int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
                     const rt_frame* frame);
 int rt_synchronize(rt_scene* s, rt_stats* stats);
+/* rt_synchronize with the figures of every device of a multi-device scene (API 4): per_device[k] (k <
+ * capacity, may be NULL) = device k's own stats (its kernel_ms, primary_rays, ...). In *stats (may be
+ * NULL) ray counts and counters are summed over the devices and kernel_ms / trace_kernel_ms are the
+ * maximum over the devices (the frames' critical path); launches are per device. Returns the number of
+ * devices (>= 1) or a negative rt_status. rt_synchronize(s, st) == rt_synchronize_devices(s, st, 0, NULL). */
+int rt_synchronize_devices(rt_scene* s, rt_stats* stats, int32_t capacity, rt_stats* per_device);
 /* copies the last frame from the device: rgb [H][W][3]; face [H][W] (-1 miss) and t [H][W] need
  * RT_FRAME_WRITE_HITS. NULL = skip. capacity_pixels: the pixels each given buffer holds; smaller than
  * the last frame's W x H -> RT_ERR_INVALID, nothing written. */

@@ -310,8 +310,13 @@ extern "C" int rt_scene_load(const char* path, const rt_scene_opts* opts, rt_sce
   if (s->opts.wide_tree) rt::build_wide(hs);  // derived from the validated binary tree (not stored)
   s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (s->opts.device != RT_DEVICE_NONE) {
-    const int rc = rt::device_upload(s.get());
+    int rc = rt::resolve_devices(s->opts);
     if (rc) return rc;
+    if ((rc = rt::device_upload(s.get()))) return rc;
+    if (s->opts.n_devices > 1 && (rc = rt::device_replicate(s.get()))) return rc;
+  } else if (s->opts.n_devices != 0) {
+    rt::set_error("rt_scene_load: a host-only scene (RT_DEVICE_NONE) lists no devices");
+    return RT_ERR_INVALID;
   }
   *out = s.release();
   return RT_OK;

@@ -3,8 +3,11 @@
 // rt_variants.hip); this file instantiates the product kernels, holds the non-template kernels (dispatch
 // order, box colours, output path, known-answer tests) and the host glue (scene upload, frame dispatch,
 // ray-list queries).
+#include <chrono>
 #include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 
 #include "rt_kernels.h"
 
@@ -142,22 +145,42 @@ __device__ __forceinline__ uint8_t ppm_u8(float c) {
   const int v = (x >= -2147483648.0f && x < 2147483648.0f) ? (int)x : INT_MIN;
   return (uint8_t)max(min(255, v), 0);
 }
+// anomaly (may be null): set when some value is NaN or negative (as k_frame_rgb8 flags it)
 __global__ __launch_bounds__(256) void k_pack_shard(const float* rgb, uint8_t* out, int W, int H, int tiles_x,
-                                                    int si, int sc, int n_tiles, int S) {
+                                                    int si, int sc, int n_tiles, int S, uint32_t* anomaly) {
   const int L = blockIdx.x;  // one block per tile slot of the shard, one thread per pixel
   if (L >= n_tiles) return;
   int tx, ty;
   shard_tile_xy(tiles_x, S, si, sc, L, tx, ty);
   const int x = tx * 16 + (threadIdx.x & 15), y = ty * 16 + (threadIdx.x >> 4);
   uint8_t* o = out + ((size_t)L * 256 + threadIdx.x) * 3;
+  bool bad = false;
   if (x < W && y < H) {
     const float* c = rgb + 3 * ((size_t)y * W + x);
-    o[0] = ppm_u8(c[0]);
-    o[1] = ppm_u8(c[1]);
-    o[2] = ppm_u8(c[2]);
+    for (int k = 0; k < 3; k++) {
+      o[k] = ppm_u8(c[k]);
+      const float x = 255.0f * c[k];  // k_frame_rgb8's test: the PPM's number (int)x below 0, or NaN
+      bad = bad || ((x >= -2147483648.0f && x < 2147483648.0f) ? (int)x : INT_MIN) < 0;
+    }
   } else {
     o[0] = o[1] = o[2] = 0;
   }
+  if (anomaly && ballot(bad) && lane_id() == 0) atomicOr(anomaly, 1u);
+}
+// Multi-device frame assembly: a replica packs its tiles' 32-bit values (ch per pixel: colour 3, face id or
+// t 1) contiguously in its shard's slot order (256 * ch words per tile, pixels outside the frame zero), so
+// one copy per device brings them to the host, which places the tiles into the caller's frame.
+__global__ __launch_bounds__(256) void k_pack_tiles32(const uint32_t* src, uint32_t* out, int W, int H, int tiles_x,
+                                                      int si, int sc, int n_tiles, int S, int ch) {
+  const int L = blockIdx.x;
+  if (L >= n_tiles) return;
+  int tx, ty;
+  shard_tile_xy(tiles_x, S, si, sc, L, tx, ty);
+  const int x = tx * 16 + (threadIdx.x & 15), y = ty * 16 + (threadIdx.x >> 4);
+  const bool in = x < W && y < H;
+  uint32_t* o = out + ((size_t)L * 256 + threadIdx.x) * ch;
+  const uint32_t* c = src + (size_t)ch * (in ? (size_t)y * W + x : 0);
+  for (int k = 0; k < ch; k++) o[k] = in ? c[k] : 0u;
 }
 __global__ __launch_bounds__(256) void k_unpack_shards(const uint8_t* packed, uint8_t* frame, int W, int H, int tiles_x,
                                                        int n, size_t slice_bytes, int S) {
@@ -218,87 +241,92 @@ void device_warmup(int device) {
   pt.mark("malloc");
 }
 
+// One pair of pinned 8-MiB staging buffers (+ their events) per device for the staged copies below, created
+// at the device's first large copy and kept for the process beside its build stream (allocating
+// and freeing pinned memory per copy can synchronise the device, stalling frames other scenes have in
+// flight, and added to the setup time). Copies to one device serialise on its staging mutex.
+struct Staging {
+  std::mutex mu;
+  void* buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
+constexpr size_t kStageChunk = 8u << 20;
+static int staging(int device, Staging** out) {
+  static Staging st[64];
+  if (device < 0 || device >= 64) { set_error("device %d out of range for staging", device); return RT_ERR_INVALID; }
+  *out = &st[device];
+  return RT_OK;
+}
+// (caller holds g.mu and has made `device` current)
+static int staging_ready(Staging& g) {
+  for (int k = 0; k < 2; k++) {
+    if (!g.buf[k]) HIPCHECK(hipHostMalloc(&g.buf[k], kStageChunk, hipHostMallocDefault));
+    if (!g.ev[k]) HIPCHECK(hipEventCreateWithFlags(&g.ev[k], hipEventDisableTiming));
+  }
+  return RT_OK;
+}
+
 int h2d(void* dst, const void* src, size_t bytes) {
-  constexpr size_t kChunk = 8u << 20;
-  if (bytes < 2 * kChunk) {
+  if (bytes < 2 * kStageChunk) {
     HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
     return RT_OK;
   }
-  struct Stage {
-    void* buf[2] = {nullptr, nullptr};
-    hipStream_t st = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    bool used[2] = {false, false};
-    ~Stage() {
-      if (st) (void)hipStreamSynchronize(st);
-      for (int k = 0; k < 2; k++) {
-        if (ev[k]) (void)hipEventDestroy(ev[k]);
-        if (buf[k]) (void)hipHostFree(buf[k]);
-      }
-    }
-  } g;
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
-  g.st = (hipStream_t)build_stream(dev);
-  if (!g.st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
-  for (int k = 0; k < 2; k++) {
-    HIPCHECK(hipHostMalloc(&g.buf[k], kChunk, hipHostMallocDefault));
-    HIPCHECK(hipEventCreateWithFlags(&g.ev[k], hipEventDisableTiming));
-  }
+  Staging* gp = nullptr;
+  int rc = staging(dev, &gp);
+  if (rc) return rc;
+  Staging& g = *gp;
+  std::lock_guard<std::mutex> lock(g.mu);
+  if ((rc = staging_ready(g))) return rc;
+  hipStream_t st = (hipStream_t)build_stream(dev);
+  if (!st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
+  // on any return the stream drains first: the staging buffers are reused by the next copy
+  struct Drain { hipStream_t st; ~Drain() { (void)hipStreamSynchronize(st); } } drain{st};
+  bool used[2] = {false, false};
   int k = 0;
-  for (size_t off = 0; off < bytes; off += kChunk, k ^= 1) {
-    const size_t n = std::min(kChunk, bytes - off);
-    if (g.used[k]) HIPCHECK(hipEventSynchronize(g.ev[k]));  // this staging buffer's previous DMA is done
+  for (size_t off = 0; off < bytes; off += kStageChunk, k ^= 1) {
+    const size_t n = std::min(kStageChunk, bytes - off);
+    if (used[k]) HIPCHECK(hipEventSynchronize(g.ev[k]));  // this staging buffer's previous DMA is done
     memcpy(g.buf[k], static_cast<const char*>(src) + off, n);
-    HIPCHECK(hipMemcpyAsync(static_cast<char*>(dst) + off, g.buf[k], n, hipMemcpyHostToDevice, g.st));
-    HIPCHECK(hipEventRecord(g.ev[k], g.st));
-    g.used[k] = true;
+    HIPCHECK(hipMemcpyAsync(static_cast<char*>(dst) + off, g.buf[k], n, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipEventRecord(g.ev[k], st));
+    used[k] = true;
   }
-  HIPCHECK(hipStreamSynchronize(g.st));
+  HIPCHECK(hipStreamSynchronize(st));
   return RT_OK;
 }
 
 // Device -> host copy into pageable memory, the same way round: DMA into one pinned 8-MiB staging buffer
 // while the host copies the other out (the device builders' read-backs).
 int d2h(void* dst, const void* src, size_t bytes) {
-  constexpr size_t kChunk = 8u << 20;
-  if (bytes < 2 * kChunk) {
+  if (bytes < 2 * kStageChunk) {
     HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return RT_OK;
   }
-  struct Stage {
-    void* buf[2] = {nullptr, nullptr};
-    hipStream_t st = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    ~Stage() {
-      if (st) (void)hipStreamSynchronize(st);
-      for (int k = 0; k < 2; k++) {
-        if (ev[k]) (void)hipEventDestroy(ev[k]);
-        if (buf[k]) (void)hipHostFree(buf[k]);
-      }
-    }
-  } g;
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
-  g.st = (hipStream_t)build_stream(dev);
-  if (!g.st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
-  for (int k = 0; k < 2; k++) {
-    HIPCHECK(hipHostMalloc(&g.buf[k], kChunk, hipHostMallocDefault));
-    HIPCHECK(hipEventCreateWithFlags(&g.ev[k], hipEventDisableTiming));
-  }
-  const size_t nchunks = (bytes + kChunk - 1) / kChunk;
+  Staging* gp = nullptr;
+  int rc = staging(dev, &gp);
+  if (rc) return rc;
+  Staging& g = *gp;
+  std::lock_guard<std::mutex> lock(g.mu);
+  if ((rc = staging_ready(g))) return rc;
+  hipStream_t st = (hipStream_t)build_stream(dev);
+  if (!st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
+  struct Drain { hipStream_t st; ~Drain() { (void)hipStreamSynchronize(st); } } drain{st};
+  const size_t nchunks = (bytes + kStageChunk - 1) / kStageChunk;
   auto issue = [&](size_t c) -> int {
-    const size_t off = c * kChunk, n = std::min(kChunk, bytes - off);
-    HIPCHECK(hipMemcpyAsync(g.buf[c & 1], static_cast<const char*>(src) + off, n, hipMemcpyDeviceToHost, g.st));
-    HIPCHECK(hipEventRecord(g.ev[c & 1], g.st));
+    const size_t off = c * kStageChunk, n = std::min(kStageChunk, bytes - off);
+    HIPCHECK(hipMemcpyAsync(g.buf[c & 1], static_cast<const char*>(src) + off, n, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipEventRecord(g.ev[c & 1], st));
     return RT_OK;
   };
-  int rc = issue(0);
-  if (rc) return rc;
+  if ((rc = issue(0))) return rc;
   for (size_t c = 0; c < nchunks; c++) {
     if (c + 1 < nchunks && (rc = issue(c + 1))) return rc;  // the next chunk's DMA overlaps this copy-out
     HIPCHECK(hipEventSynchronize(g.ev[c & 1]));
-    const size_t off = c * kChunk, n = std::min(kChunk, bytes - off);
+    const size_t off = c * kStageChunk, n = std::min(kStageChunk, bytes - off);
     memcpy(static_cast<char*>(dst) + off, g.buf[c & 1], n);
   }
   return RT_OK;
@@ -311,6 +339,22 @@ static int dalloc_copy(T** dst, const void* src, size_t bytes, int64_t& total) {
   HIPCHECK(hipMalloc((void**)dst, bytes));
   total += (int64_t)bytes;
   if (src) return h2d(*dst, src, bytes);
+  return RT_OK;
+}
+
+static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // what dalloc_copy allocates
+
+// the scene's device and its frame-slot streams (one per frame in flight)
+static int init_slots(rt_scene* s, int dev) {
+  HIPCHECK(hipSetDevice(dev));
+  s->device = dev;
+  s->n_slots = std::max(1, std::min((int)s->opts.frames_in_flight, (int)rt_scene::kMaxSlots));
+  for (int k = 0; k < s->n_slots; k++) {
+    hipStream_t st;
+    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    s->slots[k].stream = st;
+  }
+  s->stream = s->slots[0].stream;
   return RT_OK;
 }
 
@@ -330,20 +374,12 @@ int device_upload(rt_scene* s) {
   int dev = s->opts.device;
   if (dev < 0) HIPCHECK(hipGetDevice(&dev));
   if (dev >= ndev) { set_error("device %d out of range (%d devices)", dev, ndev); return RT_ERR_INVALID; }
-  HIPCHECK(hipSetDevice(dev));
-  s->device = dev;
-  s->n_slots = std::max(1, std::min((int)s->opts.frames_in_flight, (int)rt_scene::kMaxSlots));
-  for (int k = 0; k < s->n_slots; k++) {
-    hipStream_t st;
-    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    s->slots[k].stream = st;
-  }
-  s->stream = s->slots[0].stream;
+  int rc = init_slots(s, dev);
+  if (rc) return rc;
   PhaseTimer pt("upload");
   HostScene& hs = s->hs;
   int64_t& tot = s->device_bytes;
   tot = 0;
-  int rc;
   s->static_pad = scene_static_pad(hs);
   s->cert_origin_max = cert_origin_max(hs);
   pt.mark("pads");
@@ -366,6 +402,7 @@ int device_upload(rt_scene* s) {
     s->wide_base = (uint32_t)wide_base;
     s->wide_copy_bytes = wide_base ? (uint32_t)(nw * sizeof(Node128)) : 0;
     if ((rc = dalloc_copy(&s->d_nodes, nullptr, bytes, tot))) return rc;
+    s->nodes_bytes = alloc_bytes(bytes);
     pt.mark("alloc");
     // the device form of the binary records, filled on the host threads (no value-initialisation pass):
     // pad0 / pad1 = the children's record offsets (prefetch targets) with the octant order bits in their
@@ -422,6 +459,7 @@ int device_upload(rt_scene* s) {
     }
   }
   if ((rc = dalloc_copy(&s->d_nodes4, hs.nodes4.data(), hs.nodes4.size() * sizeof(Node4Q), tot))) return rc;
+  s->nodes4_bytes = alloc_bytes(hs.nodes4.size() * sizeof(Node4Q));
   {
     // per-slot shading record (float4 x 3), in the triangle records' (BVH leaf) order: the unit normals of
     // the slot's face's three vertices (Mesh normals as interpolateNormal normalises them,
@@ -444,6 +482,7 @@ int device_upload(rt_scene* s) {
     });
     pt.mark("fshade_prep");
     if ((rc = dalloc_copy(&s->d_fshade, fsh.get(), 12 * nsl * 4, tot))) return rc;
+    s->fshade_bytes = alloc_bytes(12 * nsl * 4);
     pt.mark("h2d_fshade");
   }
   std::vector<float> rb(8 * hs.boxes.size());
@@ -451,6 +490,7 @@ int device_upload(rt_scene* s) {
     for (int k = 0; k < 3; k++) { rb[8 * b + k] = hs.boxes[b].low[k]; rb[8 * b + 4 + k] = hs.boxes[b].high[k]; }
   }
   if ((rc = dalloc_copy(&s->d_refbox, rb.data(), rb.size() * 4, tot))) return rc;
+  s->refbox_bytes = alloc_bytes(rb.size() * 4);
   std::vector<DevMat> dm(hs.mats.size());
   for (size_t m = 0; m < hs.mats.size(); m++) {
     DevMat& d = dm[m];
@@ -459,20 +499,26 @@ int device_upload(rt_scene* s) {
     d.ns = hs.mats[m].shininess;
   }
   if ((rc = dalloc_copy(&s->d_mats, dm.data(), dm.size() * sizeof(DevMat), tot))) return rc;
+  s->mats_bytes = alloc_bytes(dm.size() * sizeof(DevMat));
   if ((rc = dalloc_copy(&s->d_stats, nullptr, kStatSlots * sizeof(unsigned long long), tot))) return rc;
   pt.mark("rest");
   return RT_OK;
 }
 
 void device_release(rt_scene* s) {
+  s->replicas.clear();  // each replica releases its own device state (~rt_scene)
   if (s->device == RT_DEVICE_NONE) return;
   (void)hipSetDevice(s->device);
   for (int k = 0; k < s->n_slots; k++)
     if (s->slots[k].stream) (void)hipStreamSynchronize((hipStream_t)s->slots[k].stream);
   void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_refbox, s->d_mats, s->d_stats,
-                  s->d_face_boxcolor};  // d_tris: inside d_nodes
+                  s->d_face_boxcolor, s->asm_buf.d_pack};  // d_tris: inside d_nodes
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (s->asm_buf.h_pack) (void)hipHostFree(s->asm_buf.h_pack);
+  s->asm_buf = rt_scene::Assembly{};
+  s->d_nodes = nullptr; s->d_nodes4 = nullptr; s->d_tris = nullptr; s->d_fshade = nullptr;
+  s->d_refbox = nullptr; s->d_mats = nullptr; s->d_stats = nullptr;
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
     void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline, f.d_cost, f.d_order};
@@ -483,10 +529,133 @@ void device_release(rt_scene* s) {
   }
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
   s->ev_pool.clear();
+  s->ev_used = 0;
   s->stream = nullptr;
   s->d_face_boxcolor = nullptr;
   s->face_boxcolor_valid = false;
+  s->device = RT_DEVICE_NONE;  // released: a second release is a no-op
 }
+
+int resolve_devices(rt_scene_opts& o) {
+  if (o.n_devices == 0) return RT_OK;
+  if (o.n_devices < RT_DEVICES_ALL || o.n_devices > RT_MAX_DEVICES) {
+    set_error("rt_scene_opts.n_devices %d outside -1..%d", o.n_devices, RT_MAX_DEVICES);
+    return RT_ERR_INVALID;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device available (the library has no CPU fallback)");
+    return RT_ERR_NO_DEVICE;
+  }
+  if (o.n_devices == RT_DEVICES_ALL) {
+    o.n_devices = std::min(ndev, (int)RT_MAX_DEVICES);
+    for (int k = 0; k < o.n_devices; k++) o.devices[k] = k;
+  }
+  for (int k = 0; k < o.n_devices; k++)
+    if (o.devices[k] < 0 || o.devices[k] >= ndev) {
+      set_error("rt_scene_opts.devices[%d] = %d: %d devices visible", k, o.devices[k], ndev);
+      return RT_ERR_INVALID;
+    }
+  o.device = o.devices[0];
+  return RT_OK;
+}
+
+// One replica: device `dst->opts.device` gets its own frame slots and a copy of src's device buffers,
+// device to device (over xGMI between GPUs with peer access; a plain device copy when both replicas share
+// a GPU). The host scene is shared (hsp), so nothing is rebuilt and nothing crosses PCIe.
+static int replicate_one(const rt_scene* src, rt_scene* dst) {
+  const int dev = dst->opts.device;
+  int rc = init_slots(dst, dev);
+  if (rc) return rc;
+  if (dev != src->device) {
+    int can = 0;
+    HIPCHECK(hipDeviceCanAccessPeer(&can, dev, src->device));
+    if (can) {
+      const hipError_t e = hipDeviceEnablePeerAccess(src->device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+      (void)hipGetLastError();  // clear an "already enabled" status
+    }
+  }
+  dst->static_pad = src->static_pad;
+  dst->cert_origin_max = src->cert_origin_max;
+  dst->wide_base = src->wide_base;
+  dst->wide_copy_bytes = src->wide_copy_bytes;
+  dst->box_colors = src->box_colors;
+  hipStream_t st = (hipStream_t)build_stream(dev);
+  if (!st) { set_error("no build stream on device %d", dev); return RT_ERR_HIP; }
+  struct Drain { hipStream_t st; ~Drain() { (void)hipStreamSynchronize(st); } } drain{st};
+  int64_t& tot = dst->device_bytes;
+  tot = 0;
+  auto copy = [&](auto** d, const void* sp, size_t bytes) -> int {
+    HIPCHECK(hipMalloc((void**)d, bytes));
+    tot += (int64_t)bytes;
+    if (dev == src->device) HIPCHECK(hipMemcpyAsync(*d, sp, bytes, hipMemcpyDeviceToDevice, st));
+    else HIPCHECK(hipMemcpyPeerAsync(*d, dev, sp, src->device, bytes, st));
+    return RT_OK;
+  };
+  if ((rc = copy(&dst->d_nodes, src->d_nodes, src->nodes_bytes))) return rc;
+  dst->d_tris = reinterpret_cast<TriRec64*>(reinterpret_cast<char*>(dst->d_nodes) +
+                                            (reinterpret_cast<const char*>(src->d_tris) - reinterpret_cast<const char*>(src->d_nodes)));
+  if ((rc = copy(&dst->d_nodes4, src->d_nodes4, src->nodes4_bytes))) return rc;
+  if ((rc = copy(&dst->d_fshade, src->d_fshade, src->fshade_bytes))) return rc;
+  if ((rc = copy(&dst->d_refbox, src->d_refbox, src->refbox_bytes))) return rc;
+  if ((rc = copy(&dst->d_mats, src->d_mats, src->mats_bytes))) return rc;
+  dst->nodes_bytes = src->nodes_bytes;
+  dst->nodes4_bytes = src->nodes4_bytes;
+  dst->fshade_bytes = src->fshade_bytes;
+  dst->refbox_bytes = src->refbox_bytes;
+  dst->mats_bytes = src->mats_bytes;
+  HIPCHECK(hipMalloc((void**)&dst->d_stats, kStatSlots * sizeof(unsigned long long)));
+  tot += (int64_t)(kStatSlots * sizeof(unsigned long long));
+  HIPCHECK(hipStreamSynchronize(st));
+  return RT_OK;
+}
+
+int device_replicate(rt_scene* s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  s->replicas.clear();
+  const int D = s->opts.n_devices;
+  for (int k = 1; k < D; k++) {
+    std::unique_ptr<rt_scene> r(new rt_scene(s->hsp));
+    r->opts = s->opts;
+    r->opts.n_devices = 0;
+    r->opts.device = s->opts.devices[k];
+    r->builder_used = s->builder_used;
+    r->box_builder_used = s->box_builder_used;
+    s->replicas.push_back(std::move(r));
+  }
+  // one host thread per replica (each makes its device current and copies from device 0's buffers)
+  std::vector<int> rcs(s->replicas.size(), RT_OK);
+  std::vector<std::string> errs(s->replicas.size());
+  std::vector<std::thread> workers;
+  for (size_t k = 0; k < s->replicas.size(); k++) {
+    auto job = [&, k] {
+      rcs[k] = replicate_one(s, s->replicas[k].get());
+      if (rcs[k]) errs[k] = rt_last_error();
+    };
+    try {
+      workers.emplace_back(job);
+    } catch (const std::exception&) {
+      job();  // no helper thread: copy on this one
+    }
+  }
+  for (auto& w : workers) w.join();
+  (void)hipSetDevice(s->device);
+  for (size_t k = 0; k < rcs.size(); k++)
+    if (rcs[k]) {
+      set_error("replicating the scene to device %d: %s", s->opts.devices[k + 1], errs[k].c_str());
+      s->replicas.clear();
+      return rcs[k];
+    }
+  s->replicate_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return RT_OK;
+}
+
+}  // namespace rt
+
+rt_scene::~rt_scene() { rt::device_release(this); }
+
+namespace rt {
 
 // RT_MODE_BOX_COLORS: (re)computes the per-face box-colour sums when the colours changed. The scene's
 // streams are drained first (earlier box-colour frames in flight read the table).
@@ -724,8 +893,8 @@ extern "C" int rt_device_count(void) {
 // the process environment or the kernel variant.
 static int frame_super_tile(int shard_count) { return shard_count > 1 ? kShardSuperTile : 1; }
 
-extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
-                               const rt_frame* fr) {
+// one device's share of a frame (the whole frame on a single-device scene; a replica's shard otherwise)
+static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights, const rt_frame* fr) {
   int rc = check_device_scene(s);
   if (rc) return rc;
   if (!cam || !fr || fr->width <= 0 || fr->height <= 0 || n_lights < 0 || n_lights > RT_MAX_LIGHTS ||
@@ -1041,7 +1210,7 @@ extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light
   return RT_OK;
 }
 
-extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
+static int sync_one(rt_scene* s, rt_stats* out) {
   int rc = check_device_scene(s);
   if (rc) return rc;
   for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
@@ -1083,9 +1252,201 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
   return RT_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Multi-device scenes (rt_scene_opts.n_devices > 1): one frame over the scene's replicas
+// ------------------------------------------------------------------------------------------------
+static rt_scene* replica(rt_scene* s, int k) { return k == 0 ? s : s->replicas[(size_t)k - 1].get(); }
+static int n_replicas(const rt_scene* s) { return 1 + (int)s->replicas.size(); }
+
+// The caller's frame (shard si of sc, normally the whole frame) goes to the D replicas as shards of an
+// sc*D-way split: replica k renders shard si + sc*k, so the D shards together are exactly the caller's
+// shard (super-tile t: t % (sc*D) = si + sc*k  <=>  t % sc = si). Each replica renders on its own slot
+// streams, the launches of all devices queued from this thread; nothing is exchanged between devices.
+static int render_multi(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights, const rt_frame* fr) {
+  if (!fr) { set_error("rt_render: invalid arguments"); return RT_ERR_INVALID; }
+  const int D = n_replicas(s);
+  const int sc = fr->shard_count > 0 ? fr->shard_count : 1, si = fr->shard_index;
+  if (si < 0 || si >= sc) { set_error("rt_render: shard %d of %d", si, sc); return RT_ERR_INVALID; }
+  if ((int64_t)sc * D > (1 << 24)) { set_error("rt_render: %d shards x %d devices", sc, D); return RT_ERR_INVALID; }
+  for (int k = 0; k < D; k++) {
+    rt_frame f = *fr;
+    f.shard_count = sc * D;
+    f.shard_index = si + sc * k;
+    const int rc = render_one(replica(s, k), cam, lights, n_lights, &f);
+    if (rc) return rc;
+  }
+  HIPCHECK(hipSetDevice(s->device));
+  return RT_OK;
+}
+
+extern "C" int rt_render_async(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights,
+                               const rt_frame* fr) {
+  if (s && !s->replicas.empty()) return render_multi(s, cam, lights, n_lights, fr);
+  return render_one(s, cam, lights, n_lights, fr);
+}
+
+extern "C" int rt_synchronize_devices(rt_scene* s, rt_stats* out, int32_t capacity, rt_stats* per_device) {
+  if (!s) { set_error("null scene"); return RT_ERR_INVALID; }
+  const int D = n_replicas(s);
+  rt_stats tot;
+  memset(&tot, 0, sizeof tot);
+  int first_rc = RT_OK;
+  for (int k = 0; k < D; k++) {  // every device is drained, even after a failure on one of them
+    rt_stats st;
+    const int rc = sync_one(replica(s, k), &st);
+    if (rc) {
+      if (first_rc == RT_OK) first_rc = rc;
+      continue;
+    }
+    if (per_device && k < capacity) per_device[k] = st;
+    tot.kernel_ms = std::max(tot.kernel_ms, st.kernel_ms);
+    tot.trace_kernel_ms = std::max(tot.trace_kernel_ms, st.trace_kernel_ms);
+    tot.launches = std::max(tot.launches, st.launches);
+    tot.primary_rays += st.primary_rays;
+    tot.total_rays += st.total_rays;
+    tot.hits += st.hits;
+    tot.node_visits += st.node_visits;
+    tot.tri_tests += st.tri_tests;
+    tot.wave_node_fetches += st.wave_node_fetches;
+    tot.wave_tri_fetches += st.wave_tri_fetches;
+    tot.wave_node_bytes += st.wave_node_bytes;
+  }
+  if (D > 1 && s->device != RT_DEVICE_NONE) (void)hipSetDevice(s->device);
+  if (first_rc) return first_rc;
+  if (out) *out = tot;
+  return D;
+}
+
+extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
+  const int rc = rt_synchronize_devices(s, out, 0, nullptr);
+  return rc < 0 ? rc : RT_OK;
+}
+
+// Frame assembly of a multi-device scene: every replica packs its tiles of its last frame (contiguous, its
+// shard's slot order: k_pack_tiles32 / k_pack_shard) and copies them into its pinned host buffer, all
+// devices queued first; then one host worker per device waits for its copy and places the tiles into the
+// caller's frame (rows of 16 pixels). Only the tiles of the replicas' shards are written.
+enum AsmKind { ASM_RGB = 0, ASM_FACE = 1, ASM_T = 2, ASM_RGB8 = 3 };
+static int assemble(rt_scene* s, AsmKind kind, int64_t capacity_pixels, void* out, int32_t* exact, const char* what) {
+  const int D = n_replicas(s);
+  const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
+  const size_t E = kind == ASM_RGB ? 12 : kind == ASM_RGB8 ? 3 : 4;  // bytes per pixel
+  if (W <= 0 || H <= 0) { set_error("%s: no frame rendered", what); return RT_ERR_INVALID; }
+  if (capacity_pixels < (int64_t)W * H) {
+    set_error("%s: buffers hold %lld pixels, the last frame has %lld (%d x %d)", what, (long long)capacity_pixels,
+              (long long)W * H, W, H);
+    return RT_ERR_INVALID;
+  }
+  struct Job {
+    rt_scene* r;
+    int si, sc, S, n_tiles;
+    size_t bytes, flag_off;
+  };
+  std::vector<Job> jobs((size_t)D);
+  for (int k = 0; k < D; k++) {
+    rt_scene* r = replica(s, k);
+    int rc = check_device_scene(r);
+    if (rc) return rc;
+    rt_scene::FrameSlot& f = r->slots[r->last_slot];
+    if (!f.d_rgb || r->last_W != W || r->last_H != H || (size_t)W * H > f.fb_pixels) {
+      set_error("%s: device %d has no frame of the scene's last size", what, r->device);
+      return RT_ERR_INVALID;
+    }
+    if ((kind == ASM_FACE || kind == ASM_T) && !(r->last_flags & RT_FRAME_WRITE_HITS)) {
+      set_error("last frame was rendered without RT_FRAME_WRITE_HITS");
+      return RT_ERR_INVALID;
+    }
+    Job& j = jobs[k];
+    j.r = r;
+    j.si = r->last_shard_index;
+    j.sc = r->last_shard_count;
+    j.S = frame_super_tile(j.sc);
+    j.n_tiles = shard_tile_slots(tiles_x, tiles_y, j.S, j.si, j.sc);
+    j.bytes = (size_t)j.n_tiles * 256 * E;
+    j.flag_off = (j.bytes + 15) & ~(size_t)15;
+    const size_t need = j.flag_off + 16;
+    hipStream_t st = (hipStream_t)f.stream;
+    rt_scene::Assembly& a = r->asm_buf;
+    if (need > a.bytes) {
+      HIPCHECK(hipStreamSynchronize(st));
+      if (a.d_pack) (void)hipFree(a.d_pack);
+      if (a.h_pack) (void)hipHostFree(a.h_pack);
+      a = rt_scene::Assembly{};
+      HIPCHECK(hipMalloc(&a.d_pack, need));
+      HIPCHECK(hipHostMalloc(&a.h_pack, need, hipHostMallocDefault));
+      a.bytes = need;
+    }
+    uint32_t* flag = (uint32_t*)((char*)a.d_pack + j.flag_off);
+    if (j.n_tiles > 0) {
+      if (kind == ASM_RGB8) {
+        HIPCHECK(hipMemsetAsync(flag, 0, 4, st));
+        hipLaunchKernelGGL(k_pack_shard, dim3(j.n_tiles), dim3(256), 0, st, (const float*)f.d_rgb, (uint8_t*)a.d_pack, W,
+                           H, tiles_x, j.si, j.sc, j.n_tiles, j.S, flag);
+      } else {
+        const uint32_t* src = kind == ASM_RGB ? (const uint32_t*)f.d_rgb
+                              : kind == ASM_FACE ? (const uint32_t*)f.d_face : (const uint32_t*)f.d_t;
+        hipLaunchKernelGGL(k_pack_tiles32, dim3(j.n_tiles), dim3(256), 0, st, src, (uint32_t*)a.d_pack, W, H, tiles_x,
+                           j.si, j.sc, j.n_tiles, j.S, kind == ASM_RGB ? 3 : 1);
+      }
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(a.h_pack, a.d_pack, kind == ASM_RGB8 ? need : j.bytes, hipMemcpyDeviceToHost, st));
+    }
+  }
+  // host workers: device k's tiles into the caller's frame once its copy has landed
+  std::vector<int> rcs((size_t)D, RT_OK);
+  std::vector<std::string> errs((size_t)D);
+  std::vector<uint32_t> flags((size_t)D, 0);
+  auto place = [&](int k) {
+    const Job& j = jobs[k];
+    if (hipSetDevice(j.r->device) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)j.r->slots[j.r->last_slot].stream) != hipSuccess) {
+      rcs[k] = RT_ERR_HIP;
+      errs[k] = "frame copy to the host failed";
+      return;
+    }
+    const char* src = (const char*)j.r->asm_buf.h_pack;
+    char* dst = (char*)out;
+    for (int L = 0; L < j.n_tiles; L++) {
+      int tx, ty;
+      shard_tile_xy(tiles_x, j.S, j.si, j.sc, L, tx, ty);
+      if (tx >= tiles_x || ty >= tiles_y) continue;
+      const size_t w = (size_t)std::min(16, W - tx * 16) * E;
+      const int h = std::min(16, H - ty * 16);
+      for (int yy = 0; yy < h; yy++)
+        memcpy(dst + ((size_t)(ty * 16 + yy) * W + (size_t)tx * 16) * E, src + ((size_t)L * 256 + (size_t)yy * 16) * E, w);
+    }
+    if (kind == ASM_RGB8 && j.n_tiles > 0) memcpy(&flags[k], src + j.flag_off, 4);
+  };
+  std::vector<std::thread> workers;
+  for (int k = 1; k < D; k++) {
+    try {
+      workers.emplace_back(place, k);
+    } catch (const std::exception&) {
+      place(k);
+    }
+  }
+  place(0);
+  for (auto& w : workers) w.join();
+  HIPCHECK(hipSetDevice(s->device));
+  for (int k = 0; k < D; k++)
+    if (rcs[k]) { set_error("%s: device %d: %s", what, jobs[k].r->device, errs[k].c_str()); return rcs[k]; }
+  if (exact) {
+    *exact = 1;
+    for (uint32_t fl : flags)
+      if (fl) *exact = 0;
+  }
+  return RT_OK;
+}
+
 extern "C" int rt_frame_download(rt_scene* s, int64_t capacity_pixels, float* rgb, int32_t* face, float* t) {
   int rc = check_device_scene(s);
   if (rc) return rc;
+  if (!s->replicas.empty()) {  // the devices' tiles assembled in the caller's buffers
+    if (rgb && (rc = assemble(s, ASM_RGB, capacity_pixels, rgb, nullptr, "rt_frame_download"))) return rc;
+    if (face && (rc = assemble(s, ASM_FACE, capacity_pixels, face, nullptr, "rt_frame_download"))) return rc;
+    if (t && (rc = assemble(s, ASM_T, capacity_pixels, t, nullptr, "rt_frame_download"))) return rc;
+    return RT_OK;
+  }
   const rt_scene::FrameSlot& f = s->slots[s->last_slot];
   HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));
   const size_t npix = (size_t)s->last_W * s->last_H;
@@ -1106,6 +1467,7 @@ extern "C" int rt_frame_download_rgb8(rt_scene* s, int64_t capacity_pixels, uint
   int rc = check_device_scene(s);
   if (rc) return rc;
   if (!rgb8) { set_error("rt_frame_download_rgb8: null output"); return RT_ERR_INVALID; }
+  if (!s->replicas.empty()) return assemble(s, ASM_RGB8, capacity_pixels, rgb8, exact, "rt_frame_download_rgb8");
   rt_scene::FrameSlot& f = s->slots[s->last_slot];
   const size_t npix = (size_t)s->last_W * s->last_H;
   if (!f.d_rgb || npix == 0 || npix > f.fb_pixels) { set_error("rt_frame_download_rgb8: no frame rendered"); return RT_ERR_INVALID; }
@@ -1162,6 +1524,10 @@ extern "C" int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device) {
   int rc = check_device_scene(s);
   if (rc) return rc;
   if (!dst_device) { set_error("rt_frame_pack_shard_rgb8: null destination"); return RT_ERR_INVALID; }
+  if (!s->replicas.empty()) {
+    set_error("rt_frame_pack_shard_rgb8: a multi-device scene assembles its frame itself (rt_frame_download_rgb8)");
+    return RT_ERR_UNSUPPORTED;
+  }
   rt_scene::FrameSlot& f = s->slots[s->last_slot];
   if (!f.d_rgb || (size_t)s->last_W * s->last_H > f.fb_pixels) { set_error("rt_frame_pack_shard_rgb8: no frame rendered"); return RT_ERR_INVALID; }
   const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
@@ -1172,7 +1538,7 @@ extern "C" int rt_frame_pack_shard_rgb8(rt_scene* s, void* dst_device) {
   if ((int64_t)n_tiles * 768 < slice) HIPCHECK(hipMemsetAsync((uint8_t*)dst_device + (size_t)n_tiles * 768, 0, (size_t)(slice - (int64_t)n_tiles * 768), st));
   if (n_tiles > 0)
     hipLaunchKernelGGL(k_pack_shard, dim3(n_tiles), dim3(256), 0, st, (const float*)f.d_rgb, (uint8_t*)dst_device, W, H,
-                       tiles_x, si, sc, n_tiles, S);
+                       tiles_x, si, sc, n_tiles, S, (uint32_t*)nullptr);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(st));
   return RT_OK;
@@ -1203,6 +1569,8 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* ligh
   if ((rc = rt_synchronize(s, stats))) return rc;
   if (!out_rgb) return RT_OK;
   const int W = fr->width, H = fr->height;
+  // multi-device: each device's tiles straight into the caller's frame (the rest of it untouched)
+  if (!s->replicas.empty()) return assemble(s, ASM_RGB, (int64_t)W * H, out_rgb, nullptr, "rt_render");
   const int sc = fr->shard_count > 0 ? fr->shard_count : 1;
   if (sc == 1) return rt_frame_download(s, (int64_t)W * H, out_rgb, nullptr, nullptr);
   std::vector<float> full((size_t)W * H * 3);

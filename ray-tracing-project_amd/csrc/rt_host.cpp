@@ -2191,6 +2191,15 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   if (s->opts.min_faces <= 0) s->opts.min_faces = 300;
   s->opts.frames_in_flight = std::max(1, std::min(s->opts.frames_in_flight, (int32_t)rt_scene::kMaxSlots));
   if (s->opts.max_boxes <= 0) s->opts.max_boxes = INT32_MAX;
+  if (s->opts.device == RT_DEVICE_NONE && s->opts.n_devices != 0) {
+    delete s;
+    rt::set_error("rt_scene_create: a host-only scene (RT_DEVICE_NONE) lists no devices");
+    return RT_ERR_INVALID;
+  }
+  if (s->opts.device != RT_DEVICE_NONE) {  // device list -> opts.device = devices[0] (builds and uploads there)
+    const int rc = rt::resolve_devices(s->opts);
+    if (rc) { delete s; return rc; }
+  }
   const int leaf = s->opts.leaf_size > 0 ? s->opts.leaf_size : 4;
   // the device's first-use initialisation overlaps the host preparation below (joined before the first
   // device step, or on any return)
@@ -2200,7 +2209,13 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
   } warm;
   if (s->opts.device != RT_DEVICE_NONE) {
     const int wdev = s->opts.device >= 0 ? s->opts.device : rt::current_device();
-    if (wdev >= 0) warm.t = std::thread(rt::device_warmup, wdev);
+    if (wdev >= 0) {
+      try {
+        warm.t = std::thread(rt::device_warmup, wdev);
+      } catch (const std::exception&) {
+        // no helper thread (resource limits): the device initialises at its first use instead
+      }
+    }
   }
   rt::HostScene& hs = s->hs;
   hs.nv = d->n_vertices;
@@ -2319,15 +2334,14 @@ extern "C" int rt_scene_create(const rt_mesh_desc* d, const rt_scene_opts* opts,
     int rc = rt::device_upload(s);
     if (rc) { delete s; return rc; }
     s->upload_ms = ms_since(t3);
+    if (s->opts.n_devices > 1 && (rc = rt::device_replicate(s))) { delete s; return rc; }
   }
   *out = s;
   return RT_OK;
 }
 
 extern "C" void rt_scene_destroy(rt_scene* s) {
-  if (!s) return;
-  rt::device_release(s);
-  delete s;
+  delete s;  // ~rt_scene releases the device replicas and this scene's device state (rt_device.hip)
 }
 
 extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
@@ -2339,6 +2353,9 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* o) {
   o->bvh_leaves = s->hs.leaves;
   o->bvh_depth = s->hs.depth;
   o->device_bytes = s->device_bytes;
+  for (const auto& r : s->replicas) o->device_bytes += r->device_bytes;
+  o->n_devices = s->device == RT_DEVICE_NONE ? 0 : 1 + (int32_t)s->replicas.size();
+  o->replicate_ms = s->replicate_ms;
   o->build_ms = s->build_ms;
   o->device = s->device;
   o->prep_ms = s->prep_ms;
@@ -2380,6 +2397,10 @@ extern "C" int rt_scene_set_box_colors(rt_scene* s, const float* colors3) {
   else rt_box_colors_random(nb, nullptr, c.data());
   // frames in flight may still read the per-face table: it is rebuilt at the next box-colour frame,
   // after the scene's streams have drained (rt_device.hip: ensure_face_boxcolor)
+  for (auto& r : s->replicas) {  // every device of a multi-device scene renders with the same colours
+    r->box_colors = c;
+    r->face_boxcolor_valid = false;
+  }
   s->box_colors.swap(c);
   s->face_boxcolor_valid = false;
   return RT_OK;

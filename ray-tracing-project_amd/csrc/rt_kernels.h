@@ -103,6 +103,13 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+// The lane id recomputed where it is needed (v_mbcnt; volatile, so the compiler cannot reuse the entry's
+// thread id and keep it live across the traversal -- in the FULL megakernel that value was spilled).
+__device__ __forceinline__ uint32_t lane_id_fresh() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 
 // counters of the RT_FRAME_STATS counting run
 // ST_WPOP / ST_WCULL (counting run, closest hit): stack pops per wave, and those pops at which no lane
@@ -1411,10 +1418,18 @@ constexpr int kFullWPB = 1;
 template <bool STATS, bool HITS, int TRAV, int WPE = kFullWavesPerEu>
 __global__ __launch_bounds__(64 * kFullWPB) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_render_full(FrameParams P) {
+  static_assert(kFullWPB == 1, "the pixel words below are per one-wave block");
   __shared__ WaveLds<TRAV, STATS> lds;
+  // the lane's pixel (x, y; x = ~0 when inactive), parked in LDS across the traversal and re-read by a
+  // freshly computed lane id at the end: held in registers, the thread id and the pixel coordinates were
+  // spilled to scratch (16 B per lane written at every pixel: ~33 MB of HBM writes per 1080p frame
+  // against the 24.9 MB frame itself)
+  __shared__ uint32_t pix_xy[2][64];
   wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<kFullWPB>(P);
   const bool active = c.active;
+  pix_xy[0][c.lane] = active ? (uint32_t)c.px : 0xFFFFFFFFu;
+  pix_xy[1][c.lane] = (uint32_t)c.py;
   uint32_t cnt[ST_COUNT] = {};
   const Ray r = primary_ray(P, c.px, c.py);
   if (STATS && active) { cnt[ST_RAYS]++; cnt[ST_TOTAL]++; }
@@ -1423,8 +1438,11 @@ void k_render_full(FrameParams P) {
   uint32_t face0;
   const f3 col = trace_full<STATS, TRAV, WPE == kFullWavesPerEuSmall>(P, r, active, lds, c.slot, cnt, h, face0);
   const bool hit0 = face0 != 0xFFFFFFFFu;
-  if (active) {
-    const size_t pix = (size_t)c.py * P.W + c.px;
+  const uint32_t lane = lane_id_fresh();
+  const uint32_t px = reinterpret_cast<volatile uint32_t*>(pix_xy[0])[lane];
+  const uint32_t py = reinterpret_cast<volatile uint32_t*>(pix_xy[1])[lane];
+  if (px != 0xFFFFFFFFu) {
+    const size_t pix = (size_t)py * P.W + px;
     P.rgb[3 * pix + 0] = col.x;
     P.rgb[3 * pix + 1] = col.y;
     P.rgb[3 * pix + 2] = col.z;
@@ -1433,8 +1451,8 @@ void k_render_full(FrameParams P) {
       P.t_out[pix] = h.t;
     }
   }
-  if (STATS) flush_stats(P, cnt, c.lane);
-  wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
+  if (STATS) flush_stats(P, cnt, (int)lane);
+  wave_clock_end(P, lds.clk, (int)lane, c.qw, c.sub >= 0);
 }
 
 // traceRay(o, d, 0) for any recursion limit D = P.max_depth (flyscene.cpp:317-371; the reference fixes

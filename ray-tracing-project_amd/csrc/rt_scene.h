@@ -3,6 +3,7 @@
 #include <chrono>
 #include <cstdio>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -129,7 +130,28 @@ struct PhaseTimer {
 
 struct rt_scene {
   rt_scene_opts opts;
-  rt::HostScene hs;
+  // the host scene; shared with the scene's device replicas (one HostScene per rt_scene_create)
+  std::shared_ptr<rt::HostScene> hsp;
+  rt::HostScene& hs;
+  rt_scene() : hsp(std::make_shared<rt::HostScene>()), hs(*hsp) {}
+  explicit rt_scene(std::shared_ptr<rt::HostScene> shared) : hsp(std::move(shared)), hs(*hsp) {}
+  ~rt_scene();  // releases the replicas and this scene's device state (rt_device.hip)
+  rt_scene(const rt_scene&) = delete;
+  rt_scene& operator=(const rt_scene&) = delete;
+  // Multi-device scenes (rt_scene_opts.n_devices > 1): this scene is device 0's replica; replicas[k - 1]
+  // renders on opts.devices[k] with its own copy of the device data (peer copies of this scene's buffers)
+  // and its own frame slots. A frame's tiles are split over the replicas as shards (rt_device.hip
+  // render_multi); each replica packs its tiles and copies them into pinned host memory for assembly.
+  std::vector<std::unique_ptr<rt_scene>> replicas;
+  struct Assembly {
+    void* d_pack = nullptr;  // device: this replica's tiles of the last frame, packed (rt_device.hip)
+    void* h_pack = nullptr;  // pinned host copy of it
+    size_t bytes = 0;        // capacity of both
+  } asm_buf;
+  std::vector<rt_stats> last_device_stats;  // per replica, from the last rt_synchronize of a multi-device scene
+  // device buffer sizes (peer replication copies these)
+  size_t nodes_bytes = 0, nodes4_bytes = 0, fshade_bytes = 0, refbox_bytes = 0, mats_bytes = 0;
+  double replicate_ms = 0.0;
   double build_ms = 0.0, prep_ms = 0.0, boxes_ms = 0.0, bvh_ms = 0.0, upload_ms = 0.0, bvh_gpu_ms = 0.0, boxes_gpu_ms = 0.0;
   int32_t box_builder_used = 0;
   int32_t builder_used = 0;
@@ -190,6 +212,12 @@ struct rt_scene {
 
 namespace rt {
 int device_upload(rt_scene* s);
+// Multi-device scenes: validates opts.n_devices / opts.devices (RT_DEVICES_ALL -> every visible device)
+// and writes the resolved list; n_devices 0 or 1 means a single-device scene (rt_device.hip)
+int resolve_devices(rt_scene_opts& o);
+// after device_upload of s (device opts.devices[0]): one replica per further listed device, its device
+// data peer-copied from s's (rt_device.hip)
+int device_replicate(rt_scene* s);
 int current_device();  // -1 without a GPU
 void device_release(rt_scene* s);
 }  // namespace rt

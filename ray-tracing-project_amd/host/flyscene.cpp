@@ -2,6 +2,7 @@
 // (raytraceScene); tucano/utils/flycamera.hpp (camera); all hot-path work happens in librtamd.
 #include "flyscene.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -53,6 +54,12 @@ void Flyscene::initialize(int width, int height, const std::string& obj_path, in
   o.device = device;
   o.builder = builder;
   o.box_builder = box_builder;
+  if (devices.size() == 1 && devices[0] == RT_DEVICES_ALL) {
+    o.n_devices = RT_DEVICES_ALL;
+  } else if (!devices.empty()) {
+    o.n_devices = (int32_t)std::min(devices.size(), (size_t)RT_MAX_DEVICES);
+    for (int32_t k = 0; k < o.n_devices; k++) o.devices[k] = devices[k];
+  }
   // a scene cache skips OBJ parsing and every build
   if (!cache_path.empty() && rt_scene_load(cache_path.c_str(), &o, &scene_) == RT_OK) return;
   if (rt_mesh_load_obj(obj_path.c_str(), &mesh_) != RT_OK) {

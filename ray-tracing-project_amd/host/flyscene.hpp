@@ -65,6 +65,8 @@ class Flyscene {
   std::string cache_path;                // binary scene cache: loaded if present, written after a build
   int builder = RT_BUILDER_SAH;          // RT_BUILDER_LBVH_GPU: build the BVH on the GPU
   int box_builder = RT_BOXES_HOST;       // RT_BOXES_GPU: build the reference box partition on the GPU
+  std::vector<int> devices;              // several GPUs render every frame (rt_scene_opts.devices); empty: the
+                                         // `device` of initialize(); {RT_DEVICES_ALL}: every visible GPU
 
  private:
   Flycamera flycamera;

@@ -33,7 +33,10 @@ EXPORTS = [
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
     "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
     "rt_debug_record_layout", "rt_debug_scene_flags", "rt_debug_env_knobs", "rt_debug_tree_cost",
+    "rt_synchronize_devices",
 ]
+RT_MAX_DEVICES = 16
+RT_DEVICES_ALL = -1
 
 
 class Material(C.Structure):
@@ -52,7 +55,7 @@ class SceneOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("min_faces", C.c_int32), ("max_boxes", C.c_int32),
                 ("leaf_size", C.c_int32), ("default_material", Material), ("background", C.c_float * 3),
                 ("frames_in_flight", C.c_int32), ("builder", C.c_int32), ("box_builder", C.c_int32),
-                ("wide_tree", C.c_int32)]
+                ("wide_tree", C.c_int32), ("n_devices", C.c_int32), ("devices", C.c_int32 * 16)]
 
 
 class SceneInfo(C.Structure):
@@ -61,7 +64,8 @@ class SceneInfo(C.Structure):
                 ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("device", C.c_int32),
                 ("prep_ms", C.c_double), ("boxes_ms", C.c_double), ("bvh_ms", C.c_double), ("upload_ms", C.c_double),
                 ("builder", C.c_int32), ("bvh_gpu_ms", C.c_double), ("box_builder", C.c_int32),
-                ("boxes_gpu_ms", C.c_double), ("wide_nodes", C.c_int32), ("wide_depth", C.c_int32)]
+                ("boxes_gpu_ms", C.c_double), ("wide_nodes", C.c_int32), ("wide_depth", C.c_int32),
+                ("n_devices", C.c_int32), ("replicate_ms", C.c_double)]
 
 
 class Camera(C.Structure):
@@ -132,6 +136,7 @@ def lib():
         L.rt_render.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.POINTER(Frame), vp, C.POINTER(Stats)]
         L.rt_render_async.argtypes = [vp, C.POINTER(Camera), vp, C.c_int32, C.POINTER(Frame)]
         L.rt_synchronize.argtypes = [vp, C.POINTER(Stats)]
+        L.rt_synchronize_devices.argtypes = [vp, C.POINTER(Stats), C.c_int32, vp]
         L.rt_frame_download.argtypes = [vp, C.c_int64, vp, vp, vp]
         L.rt_trace_closest.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp]
         L.rt_trace_shadow.argtypes = [vp, C.c_int32, vp, vp, vp]
@@ -290,7 +295,9 @@ RT_BOXES_HOST, RT_BOXES_GPU = 0, 1
 
 
 def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=5,
-               box_builder=1, wide_tree=0):
+               box_builder=1, wide_tree=0, devices=None):
+    """devices: None = one device (`device`); a list of HIP ordinals (repeats allowed) = a multi-device scene
+    (rt_scene_opts.n_devices / devices); RT_DEVICES_ALL = every visible device."""
     o = SceneOpts()
     lib().rt_scene_opts_default(C.byref(o))
     o.builder = builder
@@ -303,20 +310,29 @@ def scene_opts(device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, backgr
     o.leaf_size = leaf_size
     if frames_in_flight:
         o.frames_in_flight = frames_in_flight
+    if devices is not None:
+        if devices == RT_DEVICES_ALL:
+            o.n_devices = RT_DEVICES_ALL
+        else:
+            devices = list(devices)
+            if not 1 <= len(devices) <= RT_MAX_DEVICES:
+                raise ValueError(f"1..{RT_MAX_DEVICES} devices")
+            o.n_devices = len(devices)
+            o.devices[:len(devices)] = [int(d) for d in devices]
     return o
 
 
 class Scene:
     def __init__(self, mesh, device=-1, min_faces=300, leaf_size=0, frames_in_flight=0, background=None, builder=5,
-                 box_builder=1, wide_tree=0, shape_model_matrix=None):
+                 box_builder=1, wide_tree=0, shape_model_matrix=None, devices=None):
         """shape_model_matrix: the desc's getShapeModelMatrix() override (column-major 4x4), e.g. the oracle's
-        after Mesh.set_model; default the loader's normalisation."""
+        after Mesh.set_model; default the loader's normalisation. devices: see scene_opts."""
         self.mesh = mesh  # keep the mesh alive (desc borrows its arrays during create)
         self.h = C.c_void_p()
         d = mesh.desc()
         if shape_model_matrix is not None:
             d.shape_model_matrix[:] = [float(x) for x in np.asarray(shape_model_matrix, np.float32).reshape(16)]
-        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder, box_builder, wide_tree)
+        o = scene_opts(device, min_faces, leaf_size, frames_in_flight, background, builder, box_builder, wide_tree, devices)
         check(lib().rt_scene_create(C.byref(d), C.byref(o), C.byref(self.h)))
 
     def info(self):
@@ -416,12 +432,12 @@ class Scene:
         check(lib().rt_scene_save(self.h, os.fsencode(path)))
 
     @classmethod
-    def load(cls, path, device=-1, frames_in_flight=0, wide_tree=0):
+    def load(cls, path, device=-1, frames_in_flight=0, wide_tree=0, devices=None):
         """Scene from a binary cache (rt_scene_load): no OBJ parsing, no builds."""
         self = cls.__new__(cls)
         self.mesh = None
         self.h = C.c_void_p()
-        o = scene_opts(device, 300, 0, frames_in_flight, wide_tree=wide_tree)
+        o = scene_opts(device, 300, 0, frames_in_flight, wide_tree=wide_tree, devices=devices)
         check(lib().rt_scene_load(os.fsencode(path), C.byref(o), C.byref(self.h)))
         return self
 
@@ -486,6 +502,15 @@ class Scene:
         st = Stats()
         check(lib().rt_synchronize(self.h, C.byref(st)))
         return st.as_dict()
+
+    def synchronize_devices(self):
+        """rt_synchronize_devices: (totals over the devices, [per-device stats])."""
+        st = Stats()
+        per = (Stats * RT_MAX_DEVICES)()
+        n = lib().rt_synchronize_devices(self.h, C.byref(st), RT_MAX_DEVICES, per)
+        if n < 0:
+            check(n)
+        return st.as_dict(), [per[k].as_dict() for k in range(n)]
 
     def trace_closest(self, o, d):
         o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)

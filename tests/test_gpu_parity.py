@@ -491,7 +491,8 @@ def test_counting_frame_among_frames_in_flight(rt, soup):
 def test_cli_flyscene_mirror(rt, tmp_path):
     """The Flyscene-shaped host (rt_render_cli: initialize -> translate -> raytraceScene -> result.ppm):
     its PPM (8-bit download path) is byte-identical to writePPMImage of the library's float frame, also
-    when the scene comes from the binary cache or from the GPU LBVH build."""
+    when the scene comes from the binary cache or from the GPU LBVH build, and when several devices render
+    the frame in the one process (--devices: replicas sharing the test box's GPU, or every visible GPU)."""
     import subprocess
     cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ray-tracing-project_amd", "lib",
                        "rt_render_cli")
@@ -502,7 +503,8 @@ def test_cli_flyscene_mirror(rt, tmp_path):
     ref = tmp_path / "ref.ppm"
     rt.write_ppm(ref, rgb)
     cache = tmp_path / "bunny.rtscene"
-    for extra in ([], ["--cache", str(cache)], ["--cache", str(cache)], ["--lbvh", "--gpu-boxes"]):
+    for extra in ([], ["--cache", str(cache)], ["--cache", str(cache)], ["--lbvh", "--gpu-boxes"], ["--devices", "0,0"],
+                  ["--devices", "all"], ["--cache", str(cache), "--devices", "0,0,0"]):
         out = tmp_path / "out.ppm"
         subprocess.check_call([cli, obj, str(W), str(H), "--dz", "20", "--out", str(out)] + extra,
                               stdout=subprocess.DEVNULL)

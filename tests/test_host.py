@@ -20,7 +20,7 @@ def test_header_symbols_exported(rt):
     L = rt.lib()
     for name in sorted(decl):
         assert hasattr(L, name), name
-    assert L.rt_version() == 3
+    assert L.rt_version() == 4
     ident = rt.build_identity()
     assert ident["matches_tree"], ident
 
@@ -35,6 +35,32 @@ def test_no_device_is_reported_not_faked(rt):
     sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
     with pytest.raises(rt.RTError, match="host-only"):
         sc.render(rt.flycam(64, 64), rt.DEFAULT_LIGHTS, 64, 64)
+    # a multi-device scene without devices: the same loud failure, never a smaller scene
+    for devs in ([0, 1], [0, 0], rt.RT_DEVICES_ALL):
+        with pytest.raises(rt.RTError, match="no HIP device"):
+            rt.Scene(mesh, devices=devs)
+
+
+def test_device_list_rules_without_gpu(rt, tmp_path):
+    """rt_scene_opts.n_devices / devices (API 4): a host-only scene lists no devices; the list length is
+    bounded; rt_scene_load applies the same rules; the ctypes mirror has the C struct's size."""
+    import ctypes as C
+    mesh = rt.Mesh.load_obj(scene_path("cube.obj"))
+    with pytest.raises(rt.RTError, match="lists no devices"):
+        rt.Scene(mesh, device=rt.RT_DEVICE_NONE, devices=[0, 1])
+    sc = rt.Scene(mesh, device=rt.RT_DEVICE_NONE)
+    assert sc.info()["n_devices"] == 0
+    p = str(tmp_path / "cube.rtscene")
+    sc.save(p)
+    with pytest.raises(rt.RTError, match="lists no devices"):
+        rt.Scene.load(p, device=rt.RT_DEVICE_NONE, devices=[0])
+    with pytest.raises(ValueError):
+        rt.scene_opts(devices=list(range(rt.RT_MAX_DEVICES + 1)))
+    o = rt.scene_opts(devices=[3, 3, 1])
+    assert o.n_devices == 3 and list(o.devices[:3]) == [3, 3, 1]
+    # struct layout: n_devices right after wide_tree, devices[16] after it (rt_api.h)
+    assert rt.SceneOpts.n_devices.offset == rt.SceneOpts.wide_tree.offset + 4
+    assert C.sizeof(rt.SceneOpts) == rt.SceneOpts.devices.offset + 4 * rt.RT_MAX_DEVICES
 
 
 @pytest.mark.parametrize("name", SCENES)

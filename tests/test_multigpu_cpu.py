@@ -141,3 +141,23 @@ def test_gloo_scene_built_once_per_node(tmp_path):
     assert res[0][3] == 2  # RT_BUILDER_SBVH, kept by the cache
     assert len(res[0][5]) == 3 and all(x >= 0 for x in res[0][5])
     assert not os.path.exists(path)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """`python bench.py --gpus 8` without a launcher is the in-process multi-device run; with fewer visible
+    devices it must fail, never print an n_gpus 1 line. Also a launcher whose
+    WORLD_SIZE differs from --gpus."""
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["CUDA_VISIBLE_DEVICES"] = env["HIP_VISIBLE_DEVICES"] = ""  # no visible GPU, whatever the host has
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert '"n_gpus"' not in r.stdout
+    assert "visible" in r.stderr
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
