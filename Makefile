@@ -71,6 +71,12 @@ ablib: $(PKG)/csrc/rt_device.hip $(HDRS) $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OB
 	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $(PKG)/csrc/rt_variants.hip -o $(OBJ)/rt_variants_$(TAG).o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(PKG)/lib/librtamd_$(TAG).so $(OBJ)/rt_device_$(TAG).o $(OBJ)/rt_variants_$(TAG).o $(OBJ)/rt_host.o $(OBJ)/rt_cache.o $(OBJ)/rt_build.o $(OBJ)/rt_boxes.o $(OBJ)/rt_version.o -lpthread
 
+# debug build of the same sources with every scalar prefetch offset checked on the device (RT_CHECK_PREFETCH:
+# an out-of-range offset is recorded and fails the next rt_synchronize) -> lib/librtamd_pfcheck.so,
+# run the GPU suite against it with RTAMD_LIB
+pfcheck:
+	$(MAKE) ablib TAG=pfcheck EXTRA=-DRT_CHECK_PREFETCH=1
+
 cli: $(PKG)/lib/rt_render_cli
 
 $(PKG)/lib/rt_render_cli: $(PKG)/host/main.cpp $(PKG)/host/flyscene.cpp $(PKG)/host/flyscene.hpp $(LIB)
@@ -89,4 +95,4 @@ clean:
 	rm -rf $(OBJ) $(PKG)/lib
 	$(MAKE) -C oracle clean
 
-.PHONY: ablib all variants oracle cli asm clean
+.PHONY: ablib all variants oracle cli asm clean pfcheck

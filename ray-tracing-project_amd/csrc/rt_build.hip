@@ -302,11 +302,13 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
+    std::vector<hipEvent_t> evs;  // released on every return (the fallback paths included)
     ~Guard() {
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
+      for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     }
-  } g{st, {}};
+  } g{st, {}, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {
     hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
     if (e == hipSuccess) g.bufs.push_back(*p);
@@ -334,7 +336,9 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   BCHECK(hipMemsetAsync(d_flags, 0, (size_t)n * 4, st));
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
+  g.evs.push_back(e0);
   BCHECK(hipEventCreate(&e1));
+  g.evs.push_back(e1);
   BCHECK(hipEventRecord(e0, st));
   const int B = 256, G = (n + B - 1) / B;
   float3 flo = make_float3(lo[0], lo[1], lo[2]), fsc;
@@ -364,8 +368,6 @@ int gpu_build_lbvh(int device, const std::vector<TriRec64>& face_recs, const flo
   float ms = 0.0f;
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return RT_OK;
 }
 
@@ -386,11 +388,13 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
+    std::vector<hipEvent_t> evs;  // released on every return (the fallback paths included)
     ~Guard() {
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
+      for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     }
-  } g{st, {}};
+  } g{st, {}, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {
     hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
     if (e == hipSuccess) g.bufs.push_back(*p);
@@ -426,7 +430,9 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   BCHECK(hipMemsetAsync(d_cflags, 0, (size_t)n * 4, st));
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
+  g.evs.push_back(e0);
   BCHECK(hipEventCreate(&e1));
+  g.evs.push_back(e1);
   BCHECK(hipEventRecord(e0, st));
   const int B = 256, G = (n + B - 1) / B;
   float3 flo = make_float3(lo[0], lo[1], lo[2]), fsc;
@@ -481,8 +487,6 @@ int gpu_build_ploc(int device, const std::vector<TriRec64>& face_recs, const flo
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;
   if (iterations) *iterations = iters;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return RT_OK;
 }
 
@@ -1049,11 +1053,13 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   struct Guard {
     hipStream_t st;
     std::vector<void*> bufs;
+    std::vector<hipEvent_t> evs;  // released on every return (the fallback paths included)
     ~Guard() {
       (void)hipStreamSynchronize(st);
       for (void* b : bufs) (void)hipFree(b);
+      for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     }
-  } g{st, {}};
+  } g{st, {}, {}};
   auto alloc = [&](void** p, size_t bytes) -> hipError_t {
     hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
     if (e == hipSuccess) g.bufs.push_back(*p);
@@ -1093,7 +1099,9 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   pt.mark("h2d_records");
   hipEvent_t e0, e1;
   BCHECK(hipEventCreate(&e0));
+  g.evs.push_back(e0);
   BCHECK(hipEventCreate(&e1));
+  g.evs.push_back(e1);
   BCHECK(hipEventRecord(e0, st));
   const int B = kSahBlock;
   auto grid = [&](size_t k) { return dim3((unsigned)((k + B - 1) / B)); };
@@ -1205,8 +1213,6 @@ int gpu_build_sah(int device, const std::vector<TriRec64>& face_recs, const floa
   BCHECK(hipEventElapsedTime(&ms, e0, e1));
   if (gpu_ms) *gpu_ms = ms;
   if (levels) *levels = level;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   // leaves: each leaf id's references are one contiguous run of the final order
   std::vector<uint32_t> first(leaves, UINT32_MAX), count(leaves, 0);
   for (uint32_t i = 0; i < m; i++) {

@@ -501,6 +501,8 @@ int device_upload(rt_scene* s) {
   if ((rc = dalloc_copy(&s->d_mats, dm.data(), dm.size() * sizeof(DevMat), tot))) return rc;
   s->mats_bytes = alloc_bytes(dm.size() * sizeof(DevMat));
   if ((rc = dalloc_copy(&s->d_stats, nullptr, kStatSlots * sizeof(unsigned long long), tot))) return rc;
+  if ((rc = dalloc_copy(&s->d_pf_check, nullptr, 16, tot))) return rc;
+  HIPCHECK(hipMemset(s->d_pf_check, 0, 16));
   pt.mark("rest");
   return RT_OK;
 }
@@ -512,13 +514,13 @@ void device_release(rt_scene* s) {
   for (int k = 0; k < s->n_slots; k++)
     if (s->slots[k].stream) (void)hipStreamSynchronize((hipStream_t)s->slots[k].stream);
   void* bufs[] = {s->d_nodes, s->d_nodes4, s->d_fshade, s->d_refbox, s->d_mats, s->d_stats,
-                  s->d_face_boxcolor, s->asm_buf.d_pack};  // d_tris: inside d_nodes
+                  s->d_face_boxcolor, s->asm_buf.d_pack, s->d_pf_check};  // d_tris: inside d_nodes
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (s->asm_buf.h_pack) (void)hipHostFree(s->asm_buf.h_pack);
   s->asm_buf = rt_scene::Assembly{};
   s->d_nodes = nullptr; s->d_nodes4 = nullptr; s->d_tris = nullptr; s->d_fshade = nullptr;
-  s->d_refbox = nullptr; s->d_mats = nullptr; s->d_stats = nullptr;
+  s->d_refbox = nullptr; s->d_mats = nullptr; s->d_stats = nullptr; s->d_pf_check = nullptr;
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
     void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline, f.d_cost, f.d_order};
@@ -607,6 +609,9 @@ static int replicate_one(const rt_scene* src, rt_scene* dst) {
   dst->mats_bytes = src->mats_bytes;
   HIPCHECK(hipMalloc((void**)&dst->d_stats, kStatSlots * sizeof(unsigned long long)));
   tot += (int64_t)(kStatSlots * sizeof(unsigned long long));
+  HIPCHECK(hipMalloc((void**)&dst->d_pf_check, 16));
+  HIPCHECK(hipMemsetAsync(dst->d_pf_check, 0, 16, st));
+  tot += 16;
   HIPCHECK(hipStreamSynchronize(st));
   return RT_OK;
 }
@@ -710,6 +715,10 @@ static void fill_scene_params(const rt_scene* s, FrameParams& P) {
   P.sc.cert_origin_max = s->cert_origin_max;
   P.sc.wide_base = s->wide_base;
   P.sc.wide_copy_bytes = s->wide_copy_bytes;
+  P.sc.rec_bytes = (uint32_t)((hs.nodes.size() + hs.tris.size()) * 64);
+  P.sc.tri_bytes = (uint32_t)(hs.tris.size() * 64);
+  P.sc.all_bytes = (uint32_t)std::min<size_t>(s->nodes_bytes, 0xFFFFFFFFu);
+  P.sc.pf_check = s->d_pf_check;
   memcpy(P.sc.Minv, hs.Minv, 64);
   memcpy(P.Minv, hs.Minv, 64);
   memcpy(P.MS, hs.MS, 36);
@@ -1210,10 +1219,26 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   return RT_OK;
 }
 
+// RT_CHECK_PREFETCH debug build: an out-of-range scalar prefetch offset recorded by the kernels fails the call
+static int check_prefetch_word(rt_scene* s) {
+#ifdef RT_CHECK_PREFETCH
+  uint32_t w = 0;
+  HIPCHECK(hipMemcpy(&w, s->d_pf_check, 4, hipMemcpyDeviceToHost));
+  if (w) {
+    set_error("RT_CHECK_PREFETCH: out-of-range scalar load offset (sites 0x%x: 0 node, 1/2 child prefetch, 3 leaf "
+              "prefetch, 4 wide prefetch, 5 wide node)", w);
+    return RT_ERR_HIP;
+  }
+#endif
+  (void)s;
+  return RT_OK;
+}
+
 static int sync_one(rt_scene* s, rt_stats* out) {
   int rc = check_device_scene(s);
   if (rc) return rc;
   for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
+  if ((rc = check_prefetch_word(s))) return rc;
   struct Reset {
     rt_scene* s;
     ~Reset() {
@@ -1664,6 +1689,7 @@ static int trace_rays(rt_scene* s, int query, int32_t n, const float* o, const f
   }
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(st));
+  if ((rc = check_prefetch_word(s))) return rc;
   if (query == Q_SHADOW) {
     HIPCHECK(hipMemcpy(blocked, R.blocked, (size_t)n * 4, hipMemcpyDeviceToHost));
   } else {

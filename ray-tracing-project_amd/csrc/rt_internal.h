@@ -166,6 +166,12 @@ struct DevScene {
   int32_t n_nodes;
   float Minv[16];          // getShapeModelMatrix().inverse() (object-space hit point for the box fast path)
   float cert_origin_max;   // kBoxCertBit holds for rays whose object-space origin has max norm <= this
+  // Byte ranges of the scalar prefetches (checked only in the RT_CHECK_PREFETCH debug build, `make pfcheck`):
+  // node / child-prefetch offsets from `nodes` stay below rec_bytes (binary nodes + triangle records),
+  // leaf-prefetch offsets from `tris` below tri_bytes, wide-tree offsets from `nodes` below all_bytes; a
+  // violation sets bit <site> of *pf_check (and the load reads offset 0 instead)
+  uint32_t rec_bytes, tri_bytes, all_bytes;
+  uint32_t* pf_check;
 };
 
 // hit information handed between FULL stage kernels (32 B); face == 0xFFFFFFFF: no hit

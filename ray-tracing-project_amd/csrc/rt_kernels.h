@@ -82,10 +82,24 @@ __device__ __forceinline__ Node64 sload_node(const Node64* base, uint32_t h) { r
 // its own (the caller waits once at the end of the traversal). The ray's reciprocal direction, passed
 // through the prefetch asm as a read-write operand (a loop-carried copy, no move), keeps the box tests
 // below it.
-__device__ __forceinline__ Node64 sload_node_pf_inreg(const Node64* base, uint32_t h, uint32_t& pf0, uint32_t& pf1,
+// Prefetch-offset check of the RT_CHECK_PREFETCH debug build (`make pfcheck`, DESIGN.md section 5 "scalar
+// prefetch offsets"): an offset at or above its limit is recorded in bit `site` of *check and replaced by 0
+// (a valid record), so a GPU run of the test suite with that build shows that no product loop issues an
+// out-of-range scalar load -- without faulting the GPU. The product build compiles this to the offset.
+__device__ __forceinline__ uint32_t pf_off(uint32_t off, uint32_t limit, uint32_t* check, int site) {
+#ifdef RT_CHECK_PREFETCH
+  if (off >= limit) {
+    atomicOr(check, 1u << site);  // (a vector atomic from every active lane)
+    return 0u;
+  }
+#endif
+  (void)limit, (void)check, (void)site;
+  return off;
+}
+__device__ __forceinline__ Node64 sload_node_pf_inreg(const DevScene& P, uint32_t h, uint32_t& pf0, uint32_t& pf1,
                                                       f3& id) {
-  const uint32_t off = node_offset(__builtin_amdgcn_readfirstlane(h));
-  const uint64_t b = (uint64_t)base;
+  const uint32_t off = pf_off(node_offset(__builtin_amdgcn_readfirstlane(h)), P.rec_bytes, P.pf_check, 0);
+  const uint64_t b = (uint64_t)P.nodes;
   const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
   i16v v;
@@ -94,7 +108,7 @@ __device__ __forceinline__ Node64 sload_node_pf_inreg(const Node64* base, uint32
   __builtin_memcpy(&r, &v, 64);
   asm volatile("s_load_dword %0, %5, %6\n\ts_load_dword %1, %5, %7"
                : "+s"(pf0), "+s"(pf1), "+v"(id.x), "+v"(id.y), "+v"(id.z)
-               : "s"(bs), "s"(r.pad0), "s"(r.pad1)
+               : "s"(bs), "s"(pf_off(r.pad0, P.rec_bytes, P.pf_check, 1)), "s"(pf_off(r.pad1, P.rec_bytes, P.pf_check, 2))
                : "memory");
   return r;
 }
@@ -126,8 +140,25 @@ enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WP
        // the leaf's box (ST_WCANDM .. ST_WINSM), the triangle tests of leaves reached by descent (ST_WTRID) and
        // their entry-masked candidate count (ST_WCANDD: popped leaves unmasked), and wave-level tests where a
        // lane that never entered the leaf accepted (ST_WACCX: 0 if leaf-entry masking is exact)
-       ST_WCANDM, ST_WE1M, ST_WE2M, ST_WINSM, ST_WTRID, ST_WCANDD, ST_WACCX, ST_COUNT };
-constexpr int kStatSlots = 24;
+       ST_WCANDM, ST_WE1M, ST_WE2M, ST_WINSM, ST_WTRID, ST_WCANDD, ST_WACCX,
+       // round 5: the packet -> per-lane hybrid model. ST_HN0 .. ST_HN0 + 6: node steps
+       // by the number of lanes whose ray entered the node (bins 0, 1, 2-3, 4-7, 8-15, 16-31, 32-64);
+       // ST_HL0 .. + 6: the same for leaf visits. Per threshold k of kHybridK (3 thresholds): once the lanes
+       // entering a node fall below k, that node's subtree is a "switched region" (it ends at the first
+       // pop below the depth where it began); ST_HPN/ST_HPT + i: the packet's node steps / triangle tests
+       // inside such regions, ST_HLN/ST_HLT + i: the per-lane cost of the same regions (the maximum over the
+       // wave's lanes of the steps / tests whose node the lane entered, summed over regions) -- what a wave
+       // walking those regions one ray per lane would spend
+       ST_HN0, ST_HL0 = ST_HN0 + 7, ST_HPN = ST_HL0 + 7, ST_HPT = ST_HPN + 3, ST_HLN = ST_HPT + 3, ST_HLT = ST_HLN + 3,
+       ST_COUNT = ST_HLT + 3 };
+constexpr int kStatSlots = 64;
+static_assert(ST_COUNT <= kStatSlots, "stat slots");
+constexpr int kHybridK[3] = {4, 8, 16};
+__device__ __forceinline__ int lane_bin(uint32_t n) { return n == 0 ? 0 : n == 1 ? 1 : n < 4 ? 2 : n < 8 ? 3 : n < 16 ? 4 : n < 32 ? 5 : 6; }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
 
 struct Hit {
   float t;
@@ -404,10 +435,41 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
   uint32_t node = P.root;
   const float tmax_any = INFINITY;
   uint64_t act = ballot(active);  // lanes still tracing (wave-uniform mask)
+  // STATS, hybrid model (ST_HPN ..): per threshold, the stack depth where the current switched region began
+  // (-1: none) and this lane's node steps / triangle tests inside it
+  int hr[3] = {-1, -1, -1};
+  uint32_t hln[3] = {0, 0, 0}, hlt[3] = {0, 0, 0};
+  auto hybrid_close = [&](int depth) {  // regions that began deeper than `depth` end here
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+      if (hr[i] >= 0 && depth < hr[i]) {
+        cnt[ST_HLN + i] += wave_max_u32(hln[i]);
+        cnt[ST_HLT + i] += wave_max_u32(hlt[i]);
+        hln[i] = hlt[i] = 0;
+        hr[i] = -1;
+      }
+  };
   // one pop site and branch-free pushes keep the per-node control flow to the two uniform branches
   // (interior vs leaf, pop vs descend)
   for (;;) {
     bool pop = true;
+    if (STATS) {
+      const uint32_t nw = (uint32_t)__popcll(ballot(want) & act);
+      cnt[(is_leaf(node) ? ST_HL0 : ST_HN0) + lane_bin(nw)]++;
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        if (hr[i] < 0 && nw < (uint32_t)kHybridK[i]) hr[i] = sp;
+        if (hr[i] >= 0) {
+          if (!is_leaf(node)) {
+            cnt[ST_HPN + i]++;
+            hln[i] += want ? 1u : 0u;
+          } else {
+            cnt[ST_HPT + i] += leaf_count(node);
+            hlt[i] += want ? leaf_count(node) : 0u;
+          }
+        }
+      }
+    }
     if (!is_leaf(node)) {
       const Node64 nd = sload_node(P.nodes, node);  // one scalar 64-B fetch per wave
       if (STATS) {
@@ -473,9 +535,11 @@ __device__ __forceinline__ void traverse(const DevScene& P, const Ray& r, bool a
         desc = false;
         cnt[ST_WPOP]++;
         if (!ANY && ballot(want && tstack[sp] <= h.t) == 0) cnt[ST_WCULL]++;
+        hybrid_close(sp);  // the popped entry lies outside regions that began deeper than it
       }
     }
   }
+  if (STATS) hybrid_close(-1);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -495,9 +559,11 @@ constexpr uint32_t kPopMarker = 0xFFFFFFFFu;
 // record into a prefetch sink; the parent's prefetch already brought record 0), so that their scalar-cache
 // misses overlap one another and the first record's instead of following each test (C5 +4%, C3 unchanged:
 // profiles/ab/r04_leaf_prefetch_ab.txt). The wide loop's parent prefetch covers records 0 and 1 already.
-__device__ __forceinline__ void leaf_prefetch(uint64_t bs, uint32_t first, uint32_t from, uint32_t count, uint32_t& sink) {
+__device__ __forceinline__ void leaf_prefetch(const DevScene& P, uint64_t bs, uint32_t first, uint32_t from, uint32_t count,
+                                              uint32_t& sink) {
   for (uint32_t k = from; k < count; k++)
-    asm volatile("s_load_dword %0, %1, %2" : "+s"(sink) : "s"(bs), "s"((first + k) * 64u) : "memory");
+    asm volatile("s_load_dword %0, %1, %2" : "+s"(sink) : "s"(bs), "s"(pf_off((first + k) * 64u, P.tri_bytes, P.pf_check, 3))
+                 : "memory");
 }
 
 // the fast loop's wave-stack push as inline asm: a ds_write issued where it stands (the compiler would
@@ -525,7 +591,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
   f3 rid = r.id;  // loop-carried copy threaded through the prefetch asm
   for (;;) {
     while (!is_leaf(node)) {
-      const Node64 nd = sload_node_pf_inreg(P.nodes, node, cpf0, cpf1, rid);
+      const Node64 nd = sload_node_pf_inreg(P, node, cpf0, cpf1, rid);
       // octant loops: when both children are needed the far one is fixed by the node's order bit for
       // this octant alone, so it is chosen and pushed the moment the node has arrived -- the LDS write
       // completes under the box tests instead of delaying the next node fetch
@@ -606,7 +672,7 @@ __device__ __forceinline__ void traverse_fast_from(const DevScene& P, const Ray&
       {
         const uint64_t b = (uint64_t)P.tris;
         const uint64_t bs = ((uint64_t)uniform((uint32_t)(b >> 32)) << 32) | (uint32_t)uniform((uint32_t)b);
-        leaf_prefetch(bs, first, 1, count, cpf0);
+        leaf_prefetch(P, bs, first, 1, count, cpf0);
       }
       for (uint32_t k = 0; k < count; k++) {
         const TriRec64 tr = sload_tri(P.tris, first + k);
@@ -750,6 +816,7 @@ __device__ __forceinline__ void traverse_wide_fast(const DevScene& P, const Ray&
   // and a separate copy serves the entry after a pop, so a wait the compiler needs after the leaf path
   // (its kernel-argument reloads) stays on that path instead of heading every node step
   auto load = [&](uint32_t off, i16v& lo, i16v& hi) {
+    off = pf_off(off, P.all_bytes - 127u, P.pf_check, 5);
     asm volatile("s_load_dwordx16 %0, %3, %4\n\ts_load_dwordx16 %1, %3, %4 offset:0x40\n\ts_waitcnt lgkmcnt(0)"
                  : "=&s"(lo), "=&s"(hi), "+&s"(sink)
                  : "s"(bs), "s"(off)
@@ -768,7 +835,7 @@ __device__ __forceinline__ void traverse_wide_fast(const DevScene& P, const Ray&
       // the moment the node has arrived
       asm volatile("s_load_dword %[k], %[b], %[p0]\n\ts_load_dword %[k], %[b], %[p0] offset:0x40"
                    : [k] "+&s"(sink), "+v"(rr.id.x), "+v"(rr.id.y), "+v"(rr.id.z)
-                   : [b] "s"(bs), [p0] "s"(uniform(nd.pf[0]))
+                   : [b] "s"(bs), [p0] "s"(pf_off(uniform(nd.pf[0]), P.all_bytes - 64u, P.pf_check, 4))
                    : "memory");
       // the handles into VGPRs for the stack writes (off the masks' critical path)
       uint32_t v0 = nd.child[0], v1 = nd.child[1], v2 = nd.child[2], v3 = nd.child[3];
@@ -1410,7 +1477,10 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
 // 3 by 24% -- the traversal waits on L2 misses and needs the waves), a 6-wave bound (79 VGPR, no
 // spill) for smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident; the 5-wave bound
 // let the kernel grow to 82 VGPR = 5 waves, 4.6% slower; 7 waves spill 48 B, equal to 6).
-constexpr int kFullWavesPerEu = 8, kFullWavesPerEuSmall = 6;
+#ifndef RT_FULL_WPE_SMALL  // A/B builds only (make ablib EXTRA=-DRT_FULL_WPE_SMALL=n)
+#define RT_FULL_WPE_SMALL 6
+#endif
+constexpr int kFullWavesPerEu = 8, kFullWavesPerEuSmall = RT_FULL_WPE_SMALL;
 constexpr size_t kFullSmallSceneBytes = 32u << 20;  // 8 XCDs x 4 MiB L2
 // waves per block of the FULL megakernel (1: one 8x8 wave per block, measured +6.5% on bunny FULL and +8%
 // on the soup over 4 = one 16x16 tile per block)

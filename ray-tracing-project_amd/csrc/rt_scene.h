@@ -175,6 +175,7 @@ struct rt_scene {
   bool face_boxcolor_valid = false;
   rt::DevMat* d_mats = nullptr;
   unsigned long long* d_stats = nullptr;
+  uint32_t* d_pf_check = nullptr;  // RT_CHECK_PREFETCH debug build: out-of-range prefetch sites (DevScene::pf_check)
   int64_t device_bytes = 0;
   // frames in flight: each slot has its own stream and frame buffers (grown on demand)
   struct FrameSlot {
