@@ -656,7 +656,8 @@ def main():
             more["e2e_frame_ms"] = round(e2e, 3)
         if stats is not None:
             more["rays_per_frame_total"] = stats["total_rays"]  # primary + shadow + reflection (FULL)
-            more["total_mrays_per_s"] = round(stats["total_rays"] * n * a.steps / elapsed_max / 1e6, 2)
+            # (a rank's own rays times the ranks; a multi-device scene's stats already cover every device)
+            more["total_mrays_per_s"] = round(stats["total_rays"] * (1 if devices else n) * a.steps / elapsed_max / 1e6, 2)
         out = {
             "metric": "Mrays/s (primary) + frame ms at 1920x1080, 1M-tri BVH, 1/2/4/8 GPU",
             "value": round(value, 2),

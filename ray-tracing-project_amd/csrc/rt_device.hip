@@ -3,11 +3,14 @@
 // rt_variants.hip); this file instantiates the product kernels, holds the non-template kernels (dispatch
 // order, box colours, output path, known-answer tests) and the host glue (scene upload, frame dispatch,
 // ray-list queries).
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "rt_kernels.h"
 
@@ -344,14 +347,34 @@ static int dalloc_copy(T** dst, const void* src, size_t bytes, int64_t& total) {
 
 static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // what dalloc_copy allocates
 
-// the scene's device and its frame-slot streams (one per frame in flight)
+// The scene's device and its frame-slot streams (one per frame in flight). Each slot stream gets a hardware
+// queue of its own: an ordinary HIP stream is bound to one of a small per-process pool of queues
+// (GPU_MAX_HW_QUEUES, 4 on the boxes), shared with every other stream of the process in creation order, and two
+// slots on one queue run their frames one after the other -- measured in a fresh process: C5 with 4 frames in
+// flight 8.3 Grays/s with the slots on the pool (kernel ms per frame 0.49, two frames overlapping) against 12.3
+// when the pool had been used by two other streams first, or with 8 queues per process
+// (profiles/ab/r05_queue_probe.txt). A stream created with a CU mask is given a dedicated queue outside that
+// pool, so the slots are created with the full mask (every CU: no restriction), whatever streams the process
+// made before; a runtime that refuses falls back to an ordinary stream.
+static hipStream_t slot_stream(int dev) {
+  hipDeviceProp_t prop;
+  hipStream_t st = nullptr;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) {
+    std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) return st;
+    (void)hipGetLastError();
+    st = nullptr;
+  }
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  return st;
+}
 static int init_slots(rt_scene* s, int dev) {
   HIPCHECK(hipSetDevice(dev));
   s->device = dev;
   s->n_slots = std::max(1, std::min((int)s->opts.frames_in_flight, (int)rt_scene::kMaxSlots));
   for (int k = 0; k < s->n_slots; k++) {
-    hipStream_t st;
-    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipStream_t st = slot_stream(dev);
+    if (!st) { set_error("device %d: no stream for frame slot %d", dev, k); return RT_ERR_HIP; }
     s->slots[k].stream = st;
   }
   s->stream = s->slots[0].stream;
@@ -507,7 +530,10 @@ int device_upload(rt_scene* s) {
   return RT_OK;
 }
 
+void stop_workers(rt_scene* s);  // (below)
+
 void device_release(rt_scene* s) {
+  stop_workers(s);      // no worker touches a replica from here on
   s->replicas.clear();  // each replica releases its own device state (~rt_scene)
   if (s->device == RT_DEVICE_NONE) return;
   (void)hipSetDevice(s->device);
@@ -1116,7 +1142,8 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       // (RT_SPLIT_KP waves)
       const char* split_p_env = debug_env("RT_SPLIT_KP");
       const int split_p = split_p_env ? atoi(split_p_env) : kSplitKPrimary;
-      const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
+      // (RT_SPLIT_KP_ANY, A/B only: split lone frames of any scene size)
+      const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes || debug_env("RT_SPLIT_KP_ANY");
       P.split_k = (P.order && small_p && !P.timeline && kTraceWPB == 1)
                       ? std::max(0, std::min<int>(split_p, (int)(units / 4))) & ~7 : 0;
       if (P.cost && P.split_k)
@@ -1206,15 +1233,21 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   s->last_shard_index = si;
   s->last_shard_count = sc;
   s->last_flags = fr->flags;
-  // primary rays of this shard: pixels inside the frame of the shard's tiles
-  int64_t rays = 0;
-  for (int L = 0; L < P.n_tiles_shard; L++) {
-    int tx, ty;
-    shard_tile_xy(P.tiles_x, P.super_tile, si, sc, L, tx, ty);
-    if (tx < P.tiles_x && ty < P.tiles_y)
-      rays += (int64_t)std::min(16, fr->width - tx * 16) * std::min(16, fr->height - ty * 16);
+  // primary rays of this shard: pixels inside the frame of the shard's tiles (a walk over the shard's tiles,
+  // done once per frame shape: it is host time on every frame's enqueue path otherwise)
+  const int64_t rkey[4] = {fr->width, fr->height, si, sc};
+  if (memcmp(rkey, s->rays_key, sizeof rkey) != 0) {
+    int64_t rays = 0;
+    for (int L = 0; L < P.n_tiles_shard; L++) {
+      int tx, ty;
+      shard_tile_xy(P.tiles_x, P.super_tile, si, sc, L, tx, ty);
+      if (tx < P.tiles_x && ty < P.tiles_y)
+        rays += (int64_t)std::min(16, fr->width - tx * 16) * std::min(16, fr->height - ty * 16);
+    }
+    memcpy(s->rays_key, rkey, sizeof rkey);
+    s->rays_of_key = rays;
   }
-  s->last_rays = rays;
+  s->last_rays = s->rays_of_key;
   s->pending = true;
   return RT_OK;
 }
@@ -1283,22 +1316,142 @@ static int sync_one(rt_scene* s, rt_stats* out) {
 static rt_scene* replica(rt_scene* s, int k) { return k == 0 ? s : s->replicas[(size_t)k - 1].get(); }
 static int n_replicas(const rt_scene* s) { return 1 + (int)s->replicas.size(); }
 
+// Enqueue workers of a multi-device scene. Queueing one device's share of a frame costs ~20 us of host time
+// (frame parameters, three events, the launch); done for D devices one after the other on the caller's
+// thread that is D x 20 us per frame, which at 8 devices exceeds a device's share of the frame. So each
+// further replica has a host thread of its own: the caller posts the frame to every worker, queues replica 0
+// itself, and returns once every worker has queued its share (so errors are reported by this call and the
+// frames stay in call order on every device). A worker waits for work spinning for a while, then blocks.
+namespace rt {
+struct EnqueueWorker {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<uint32_t> posted{0}, done{0};  // job sequence numbers
+  bool quit = false;
+  rt_scene* r = nullptr;
+  rt_camera cam;
+  rt_light lights[RT_MAX_LIGHTS];
+  int32_t n_lights = 0;
+  rt_frame fr;
+  int rc = RT_OK;
+  std::string err;
+};
+
+static void worker_loop(EnqueueWorker* w) {
+  uint32_t seen = 0;
+  for (;;) {
+    // spin ~50 us for the next frame (frames come at sub-millisecond cadence), then block
+    for (int i = 0; i < 20000 && w->posted.load(std::memory_order_acquire) == seen; i++) __builtin_ia32_pause();
+    if (w->posted.load(std::memory_order_acquire) == seen) {
+      std::unique_lock<std::mutex> lk(w->mu);
+      w->cv.wait(lk, [&] { return w->quit || w->posted.load(std::memory_order_acquire) != seen; });
+    }
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      if (w->quit && w->posted.load(std::memory_order_acquire) == seen) return;
+    }
+    seen = w->posted.load(std::memory_order_acquire);
+    w->rc = render_one(w->r, &w->cam, w->n_lights ? w->lights : nullptr, w->n_lights, &w->fr);
+    if (w->rc) w->err = rt_last_error();
+    w->done.store(seen, std::memory_order_release);
+    { std::lock_guard<std::mutex> lk(w->mu); }
+    w->cv.notify_all();
+  }
+}
+
+void stop_workers(rt_scene* s) {
+  for (auto& w : s->workers) {
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->quit = true;
+    }
+    w->cv.notify_all();
+    if (w->th.joinable()) w->th.join();
+  }
+  s->workers.clear();
+}
+
+static int start_workers(rt_scene* s) {
+  if (s->workers.size() == s->replicas.size()) return RT_OK;
+  stop_workers(s);
+  for (auto& r : s->replicas) {
+    auto w = std::make_shared<EnqueueWorker>();
+    w->r = r.get();
+    try {
+      w->th = std::thread(worker_loop, w.get());
+    } catch (const std::exception&) {
+      stop_workers(s);  // no threads: the caller queues every device itself
+      return RT_ERR_UNSUPPORTED;
+    }
+    s->workers.push_back(std::move(w));
+  }
+  return RT_OK;
+}
+
+}  // namespace rt
+
 // The caller's frame (shard si of sc, normally the whole frame) goes to the D replicas as shards of an
 // sc*D-way split: replica k renders shard si + sc*k, so the D shards together are exactly the caller's
 // shard (super-tile t: t % (sc*D) = si + sc*k  <=>  t % sc = si). Each replica renders on its own slot
-// streams, the launches of all devices queued from this thread; nothing is exchanged between devices.
+// streams, its launches queued by its own worker thread (replica 0's by the caller); nothing is exchanged
+// between devices.
 static int render_multi(rt_scene* s, const rt_camera* cam, const rt_light* lights, int32_t n_lights, const rt_frame* fr) {
-  if (!fr) { set_error("rt_render: invalid arguments"); return RT_ERR_INVALID; }
+  if (!fr || !cam || n_lights < 0 || n_lights > RT_MAX_LIGHTS || (n_lights && !lights)) {
+    set_error("rt_render: invalid arguments");
+    return RT_ERR_INVALID;
+  }
   const int D = n_replicas(s);
   const int sc = fr->shard_count > 0 ? fr->shard_count : 1, si = fr->shard_index;
   if (si < 0 || si >= sc) { set_error("rt_render: shard %d of %d", si, sc); return RT_ERR_INVALID; }
   if ((int64_t)sc * D > (1 << 24)) { set_error("rt_render: %d shards x %d devices", sc, D); return RT_ERR_INVALID; }
-  for (int k = 0; k < D; k++) {
+  auto shard_of = [&](int k) {
     rt_frame f = *fr;
     f.shard_count = sc * D;
     f.shard_index = si + sc * k;
-    const int rc = render_one(replica(s, k), cam, lights, n_lights, &f);
-    if (rc) return rc;
+    return f;
+  };
+  if (start_workers(s) != RT_OK) {  // (no helper threads: queue every device from this thread)
+    for (int k = 0; k < D; k++) {
+      const rt_frame f = shard_of(k);
+      const int rc = render_one(replica(s, k), cam, lights, n_lights, &f);
+      if (rc) return rc;
+    }
+    HIPCHECK(hipSetDevice(s->device));
+    return RT_OK;
+  }
+  std::vector<uint32_t> seq(s->workers.size());
+  for (size_t k = 0; k < s->workers.size(); k++) {
+    EnqueueWorker& w = *s->workers[k];
+    {
+      std::lock_guard<std::mutex> lk(w.mu);
+      w.cam = *cam;
+      w.n_lights = n_lights;
+      if (n_lights) memcpy(w.lights, lights, sizeof(rt_light) * (size_t)n_lights);
+      w.fr = shard_of((int)k + 1);
+      seq[k] = w.posted.load(std::memory_order_relaxed) + 1;
+      w.posted.store(seq[k], std::memory_order_release);
+    }
+    w.cv.notify_all();
+  }
+  const rt_frame f0 = shard_of(0);
+  int rc = render_one(s, cam, lights, n_lights, &f0);
+  std::string err0 = rc ? rt_last_error() : "";
+  for (size_t k = 0; k < s->workers.size(); k++) {  // every worker has queued its share before this returns
+    EnqueueWorker& w = *s->workers[k];
+    for (int i = 0; i < 200000 && w.done.load(std::memory_order_acquire) != seq[k]; i++) __builtin_ia32_pause();
+    if (w.done.load(std::memory_order_acquire) != seq[k]) {
+      std::unique_lock<std::mutex> lk(w.mu);
+      w.cv.wait(lk, [&] { return w.done.load(std::memory_order_acquire) == seq[k]; });
+    }
+    if (w.rc && rc == RT_OK) {
+      rc = w.rc;
+      err0 = "device " + std::to_string(w.r->device) + ": " + w.err;
+    }
+  }
+  if (rc) {
+    set_error("%s", err0.c_str());
+    return rc;
   }
   HIPCHECK(hipSetDevice(s->device));
   return RT_OK;

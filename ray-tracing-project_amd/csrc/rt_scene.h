@@ -107,7 +107,7 @@ float scene_static_pad(const HostScene& hs);
 float cert_origin_max(const HostScene& hs);
 uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro);  // kSafeNormalBit | kBoxCertBit of face f
 void set_error(const char* fmt, ...);
-// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_LDS_PAD, RT_SAH_TRAV,
+// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_LDS_PAD, RT_SAH_TRAV,
 // RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING): getenv(name) once rt_debug_env_knobs(1) has been called,
 // else nullptr -- the product library's behaviour never depends on the caller's environment otherwise.
 const char* debug_env(const char* name);
@@ -128,6 +128,10 @@ struct PhaseTimer {
 
 }  // namespace rt
 
+namespace rt {
+struct EnqueueWorker;  // rt_device.hip: a host thread that queues one replica's share of each frame
+}
+
 struct rt_scene {
   rt_scene_opts opts;
   // the host scene; shared with the scene's device replicas (one HostScene per rt_scene_create)
@@ -143,6 +147,9 @@ struct rt_scene {
   // and its own frame slots. A frame's tiles are split over the replicas as shards (rt_device.hip
   // render_multi); each replica packs its tiles and copies them into pinned host memory for assembly.
   std::vector<std::unique_ptr<rt_scene>> replicas;
+  // one enqueue worker per replica of replicas (started at the first multi-device frame, stopped before the
+  // replicas are released): each replica's launches of a frame are queued by its own host thread
+  std::vector<std::shared_ptr<rt::EnqueueWorker>> workers;
   struct Assembly {
     void* d_pack = nullptr;  // device: this replica's tiles of the last frame, packed (rt_device.hip)
     void* h_pack = nullptr;  // pinned host copy of it
@@ -207,6 +214,7 @@ struct rt_scene {
   int n_slots = 1, next_slot = 0, last_slot = 0;
   int32_t last_W = 0, last_H = 0, last_flags = 0, last_shard_index = 0, last_shard_count = 1;
   int64_t last_rays = 0, last_total_rays = 0;
+  int64_t rays_key[4] = {-1, -1, -1, -1}, rays_of_key = 0;  // primary rays of a frame shape (W, H, shard)
   int64_t last_timeline_waves = 0;  // waves recorded by the last RT_FRAME_TIMELINE frame
   bool pending = false;
 };

@@ -20,8 +20,48 @@ for s in $STEPS; do
     pftests)
       # the whole GPU suite against the debug build whose kernels check every scalar prefetch offset
       RTAMD_LIB=$PWD/ray-tracing-project_amd/lib/librtamd_pfcheck.so timeout -k 10 600 python -u -m pytest tests -m gpu -q \
-          -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu_pfcheck.log 2>&1
+          -p no:cacheprovider --timeout 300 --timeout-method thread \
+          --deselect tests/test_gpu_parity.py::test_product_library_refuses_variant_only_kernels > $OUT/pytest_gpu_pfcheck.log 2>&1
       rc=$?; echo "pfcheck pytest rc=$rc"; tail -8 $OUT/pytest_gpu_pfcheck.log; hard $rc ;;
+    mdtests)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_multidevice.py -q -p no:cacheprovider --timeout 200 \
+          --timeout-method thread > $OUT/pytest_md.log 2>&1
+      rc=$?; echo "multidevice pytest rc=$rc"; tail -5 $OUT/pytest_md.log; hard $rc ;;
+    hybrid)
+      # the counting run's packet -> per-lane hybrid model (C3 soup, C2 bunny)
+      timeout -k 10 300 python tools/hybrid_model.py soup bunny > $OUT/hybrid_model.jsonl 2> $OUT/hybrid_model.err
+      rc=$?; echo "hybrid rc=$rc"; cat $OUT/hybrid_model.jsonl; hard $rc ;;
+    c5waves)
+      # FULL megakernel occupancy A/B (small-scene build 5 / 6 / 7 waves per SIMD), C5 in flight and alone
+      TAG=$TAG/c5waves LIBS="default w5 w7" CFGS="bunny:full:4 bunny:full:1" REPS=3 STEPS=50 timeout -k 10 900 \
+          bash tools/ablibs.sh > $OUT/c5waves.txt 2>&1
+      rc=$?; echo "c5waves rc=$rc"; cat $OUT/c5waves.txt; hard $rc ;;
+    queues)
+      # frames in flight vs hardware-queue assignment (tools/queue_probe.py), a fresh process per line
+      for sc in bunny soup; do
+        for v in ${QVARIANTS:-plain pre1 pre2 pre3 second keep2}; do
+          for f in 1 4; do
+            timeout -k 10 120 python tools/queue_probe.py $v $sc $f >> $OUT/queues.jsonl 2>> $OUT/queues.err
+            rc=$?; [ $rc -ne 0 ] && { echo "queue probe $v $sc $f rc=$rc"; hard $rc; exit $rc; }
+          done
+        done
+        GPU_MAX_HW_QUEUES=8 timeout -k 10 120 python tools/queue_probe.py plain $sc 4 >> $OUT/queues.jsonl 2>> $OUT/queues.err
+        rc=$?; [ $rc -ne 0 ] && { echo "queue probe hwq8 rc=$rc"; hard $rc; exit $rc; }
+      done
+      cat $OUT/queues.jsonl ;;
+    c3split)
+      # lone C3 frames: the costliest waves as 16-lane sub-waves also for a large scene (RT_SPLIT_KP_ANY), K waves
+      export RTAMD_DEBUG_KNOBS=1
+      for rep in 1 2; do
+        for k in none 256 512 1024 2048; do
+          if [ $k = none ]; then envs=""; else envs="RT_SPLIT_KP_ANY=1 RT_SPLIT_KP=$k"; fi
+          env $envs timeout -k 10 120 python bench.py --steps 40 --warmup 5 --no-cpu --no-side --no-extra --no-e2e \
+              --frames-in-flight 1 > $OUT/c3split_${k}_r$rep.json 2> $OUT/c3split_${k}_r$rep.err
+          rc=$?; [ $rc -ne 0 ] && { echo "c3split $k rc=$rc"; hard $rc; exit $rc; }
+          python3 -c "import json;d=json.loads(open('$OUT/c3split_${k}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('c3split $k r$rep', d['value'], d['ms_per_step'], c['kernel_ms_one_frame_alone'], d['roofline']['frac'], d['parity']['face_t_digest_equal'] if d.get('parity') else None)"
+        done
+      done
+      unset RTAMD_DEBUG_KNOBS ;;
     multi)
       # the in-process multi-device path (no launcher) with two replicas sharing the box's GPU
       timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 20 --warmup 5 > $OUT/bench_multi.json 2> $OUT/bench_multi.err
