@@ -356,26 +356,51 @@ static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // 
 // (profiles/ab/r05_queue_probe.txt). A stream created with a CU mask is given a dedicated queue outside that
 // pool, so the slots are created with the full mask (every CU: no restriction), whatever streams the process
 // made before; a runtime that refuses falls back to an ordinary stream.
-static hipStream_t slot_stream(int dev) {
+// At most kDedicatedSlotQueues such queues per device and process (two scenes' worth of slots): beyond that the
+// device's queues are oversubscribed and the hardware time-slices them -- eight replicas of one scene on one GPU
+// (32 dedicated queues) ran 2.3x slower than two (profiles/ab/r05_queue_probe.txt) -- so further slots take the
+// pool. dedicated_slots counts the live dedicated queues per device (released by release_slot_stream).
+constexpr int kDedicatedSlotQueues = 8;
+static std::mutex g_slot_mu;
+static int g_dedicated_slots[64] = {};
+static hipStream_t slot_stream(int dev, bool* dedicated) {
+  *dedicated = false;
   hipDeviceProp_t prop;
   hipStream_t st = nullptr;
-  if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) {
-    std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
-    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) return st;
-    (void)hipGetLastError();
-    st = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    if (dev >= 0 && dev < 64 && g_dedicated_slots[dev] < kDedicatedSlotQueues &&
+        hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) {
+      std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
+      if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+        g_dedicated_slots[dev]++;
+        *dedicated = true;
+        return st;
+      }
+      (void)hipGetLastError();
+      st = nullptr;
+    }
   }
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
   return st;
+}
+static void release_slot_stream(int dev, void* st, bool dedicated) {
+  if (st) (void)hipStreamDestroy((hipStream_t)st);
+  if (dedicated && dev >= 0 && dev < 64) {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    g_dedicated_slots[dev]--;
+  }
 }
 static int init_slots(rt_scene* s, int dev) {
   HIPCHECK(hipSetDevice(dev));
   s->device = dev;
   s->n_slots = std::max(1, std::min((int)s->opts.frames_in_flight, (int)rt_scene::kMaxSlots));
   for (int k = 0; k < s->n_slots; k++) {
-    hipStream_t st = slot_stream(dev);
+    bool dedicated = false;
+    hipStream_t st = slot_stream(dev, &dedicated);
     if (!st) { set_error("device %d: no stream for frame slot %d", dev, k); return RT_ERR_HIP; }
     s->slots[k].stream = st;
+    s->slots[k].dedicated_queue = dedicated;
   }
   s->stream = s->slots[0].stream;
   return RT_OK;
@@ -552,7 +577,7 @@ void device_release(rt_scene* s) {
     void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline, f.d_cost, f.d_order};
     for (void* b : fb)
       if (b) (void)hipFree(b);
-    if (f.stream) (void)hipStreamDestroy((hipStream_t)f.stream);
+    release_slot_stream(s->device, f.stream, f.dedicated_queue);
     f = rt_scene::FrameSlot{};
   }
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
@@ -1049,6 +1074,8 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   {
     const int sel = (variant >> 9) & 3;
     P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? 64 : sel == 1 ? 4 : sel == 2 ? 16 : 0);
+    const char* run_env = debug_env("RT_XCD_RUN");  // (A/B only: another run length of the chunked order)
+    if (run_env && atoi(run_env) >= 2) P.xcd_remap = atoi(run_env);
   }
   const int trav = pick_trav(P, variant);
   {
@@ -1744,11 +1771,19 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_light* ligh
                          float* out_rgb, rt_stats* stats) {
   int rc = rt_render_async(s, cam, lights, n_lights, fr);
   if (rc) return rc;
+  const int W = fr->width, H = fr->height;
+  if (!s->replicas.empty() && out_rgb) {
+    // multi-device: each device's tile packing and copy are queued right behind its share of the frame, and
+    // its host worker writes its tiles into the caller's frame as soon as that device is done (the rest of
+    // the frame untouched); the stats are collected after
+    if ((rc = assemble(s, ASM_RGB, (int64_t)W * H, out_rgb, nullptr, "rt_render"))) {
+      (void)rt_synchronize(s, nullptr);
+      return rc;
+    }
+    return rt_synchronize(s, stats);
+  }
   if ((rc = rt_synchronize(s, stats))) return rc;
   if (!out_rgb) return RT_OK;
-  const int W = fr->width, H = fr->height;
-  // multi-device: each device's tiles straight into the caller's frame (the rest of it untouched)
-  if (!s->replicas.empty()) return assemble(s, ASM_RGB, (int64_t)W * H, out_rgb, nullptr, "rt_render");
   const int sc = fr->shard_count > 0 ? fr->shard_count : 1;
   if (sc == 1) return rt_frame_download(s, (int64_t)W * H, out_rgb, nullptr, nullptr);
   std::vector<float> full((size_t)W * H * 3);

@@ -1380,8 +1380,9 @@ __global__ __launch_bounds__(256) void k_shade_primary(FrameParams P) {
 // PRIMARY as one kernel (default; variant bit 32768 selects the two-kernel form k_trace_primary +
 // k_shade_primary): the traversal, then the shading of the same lane -- the hit record stays in
 // registers instead of a round trip through HBM, and the traversal state is dead by then, so the
-// shading's registers do not add to the traversal's (64 VGPR, 8 waves/SIMD, a 112-B spill in the
-// shading part). Measured: C3 +2.7% at 4 frames in flight, bunny +4%.
+// shading's registers do not add to the traversal's. Resources of the shipped instantiation
+// k_primary_fused<false, false> (make asm -> build/asm/resource.txt, round 5): 59 VGPR, 78 SGPR, no
+// scratch, 8 waves/SIMD. Measured: C3 +2.7% at 4 frames in flight, bunny +4%.
 template <bool HITS, bool BOXCOL = false>
 __global__ __launch_bounds__(64 * kTraceWPB) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerEu)))
 void k_primary_fused(FrameParams P) {
@@ -1472,11 +1473,14 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   return col;
 }
 
-// Occupancy of the FULL megakernel, by scene: 8 waves per SIMD (64 VGPR + a 144-B spill) for scenes
-// whose node + triangle records exceed the chip's aggregate L2 (the 1M soup: 8 waves beat 5 by 18% and
-// 3 by 24% -- the traversal waits on L2 misses and needs the waves), a 6-wave bound (79 VGPR, no
-// spill) for smaller ones (bunny, C5: +14% over 8 -- their records are L2-resident; the 5-wave bound
-// let the kernel grow to 82 VGPR = 5 waves, 4.6% slower; 7 waves spill 48 B, equal to 6).
+// Occupancy of the FULL megakernel, by scene: 8 waves per SIMD for scenes whose node + triangle records
+// exceed the chip's aggregate L2 (the 1M soup: 8 waves beat 5 by 18% and 3 by 24% -- the traversal waits
+// on L2 misses and needs the waves), a 6-wave bound for smaller ones (bunny, C5: +14% over 8 -- their
+// records are L2-resident). Resources of the shipped instantiations (make asm, round 5, after the pixel
+// coordinates moved to LDS): k_render_full<false, false, 1, 6> 80 VGPR, 104 SGPR, no scratch (round 4: 80
+// VGPR + 32 B of scratch -- the spill of the thread id and px / py); <false, false, 1, 8> 64 VGPR + 96 B
+// scratch. Re-swept in round 5 without the spill: 5 waves (85 VGPR, no scratch) -1..-6%, 7 waves (72 VGPR +
+// 48 B scratch) -3..-8% against 6 (profiles/ab/r05_full_waves_ab.txt).
 #ifndef RT_FULL_WPE_SMALL  // A/B builds only (make ablib EXTRA=-DRT_FULL_WPE_SMALL=n)
 #define RT_FULL_WPE_SMALL 6
 #endif

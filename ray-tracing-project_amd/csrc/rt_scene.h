@@ -107,7 +107,7 @@ float scene_static_pad(const HostScene& hs);
 float cert_origin_max(const HostScene& hs);
 uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro);  // kSafeNormalBit | kBoxCertBit of face f
 void set_error(const char* fmt, ...);
-// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_LDS_PAD, RT_SAH_TRAV,
+// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_XCD_RUN, RT_LDS_PAD, RT_SAH_TRAV,
 // RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING): getenv(name) once rt_debug_env_knobs(1) has been called,
 // else nullptr -- the product library's behaviour never depends on the caller's environment otherwise.
 const char* debug_env(const char* name);
@@ -187,6 +187,7 @@ struct rt_scene {
   // frames in flight: each slot has its own stream and frame buffers (grown on demand)
   struct FrameSlot {
     void* stream = nullptr;
+    bool dedicated_queue = false;  // the stream has a hardware queue of its own (rt_device.hip slot_stream)
     float* d_rgb = nullptr;
     int32_t* d_face = nullptr;
     float* d_t = nullptr;

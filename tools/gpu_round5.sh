@@ -62,6 +62,51 @@ for s in $STEPS; do
         done
       done
       unset RTAMD_DEBUG_KNOBS ;;
+    multi8)
+      # eight replicas of the scene sharing the box's GPU: the in-process 8-device path end to end (enqueue workers,
+      # assembly); the rate is one GPU's, the line shows the host enqueue cost per frame and per-device figures
+      timeout -k 10 300 python bench.py --gpus 8 --devices 0,0,0,0,0,0,0,0 --steps 20 --warmup 5 --no-cpu \
+          > $OUT/bench_multi8.json 2> $OUT/bench_multi8.err
+      rc=$?; echo "multi8 rc=$rc"; cat $OUT/bench_multi8.json; hard $rc ;;
+    fifsweep)
+      # frames in flight 1-4 on the bench's own 20-step lines (C3 headline; C5 as the bench's workload), interleaved reps
+      for rep in 1 2; do
+        for sc in soup bunny; do
+          md=primary; [ $sc = bunny ] && md=full
+          for f in 1 2 3 4; do
+            timeout -k 10 120 python bench.py --scene $sc --mode $md --steps 20 --warmup 5 --no-cpu --no-side --no-extra \
+                --no-e2e --no-stats --frames-in-flight $f > $OUT/fif_${sc}_${f}_r$rep.json 2> $OUT/fif_${sc}_${f}_r$rep.err
+            rc=$?; [ $rc -ne 0 ] && { echo "fif $sc $f rc=$rc"; hard $rc; exit $rc; }
+            python3 -c "import json;d=json.loads(open('$OUT/fif_${sc}_${f}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('fif $sc f$f r$rep', d['value'], d['ms_per_step'], c['kernel_ms_per_frame'], c['kernel_ms_one_frame_alone'])"
+          done
+        done
+      done ;;
+    xcdrun)
+      # run length of the chunked XCD dispatch order (RT_XCD_RUN; product 64), C3 at 4 frames in flight and alone
+      export RTAMD_DEBUG_KNOBS=1
+      for rep in 1 2; do
+        for c in 64 32 128 256; do
+          for f in 4 1; do
+            RT_XCD_RUN=$c timeout -k 10 120 python bench.py --steps 40 --warmup 5 --no-cpu --no-side --no-extra --no-e2e \
+                --no-stats --frames-in-flight $f > $OUT/xcd_${c}_f${f}_r$rep.json 2> $OUT/xcd_${c}_f${f}_r$rep.err
+            rc=$?; [ $rc -ne 0 ] && { echo "xcd $c rc=$rc"; hard $rc; exit $rc; }
+            python3 -c "import json;d=json.loads(open('$OUT/xcd_${c}_f${f}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('xcd $c f$f r$rep', d['value'], d['ms_per_step'], c['kernel_ms_one_frame_alone'])"
+          done
+        done
+      done
+      unset RTAMD_DEBUG_KNOBS ;;
+    c5split)
+      # lone C5 frames: the K costliest waves of the longest-first order as four 16-lane sub-waves (RT_SPLIT_K; product 2048)
+      export RTAMD_DEBUG_KNOBS=1
+      for rep in 1 2; do
+        for k in 2048 1024 1536 3072; do
+          RT_SPLIT_K=$k timeout -k 10 120 python bench.py --scene bunny --mode full --steps 40 --warmup 5 --no-cpu --no-side \
+              --no-extra --no-e2e --no-stats --frames-in-flight 1 > $OUT/c5split_${k}_r$rep.json 2> $OUT/c5split_${k}_r$rep.err
+          rc=$?; [ $rc -ne 0 ] && { echo "c5split $k rc=$rc"; hard $rc; exit $rc; }
+          python3 -c "import json;d=json.loads(open('$OUT/c5split_${k}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('c5split $k r$rep', d['value'], d['ms_per_step'], c['kernel_ms_one_frame_alone'])"
+        done
+      done
+      unset RTAMD_DEBUG_KNOBS ;;
     multi)
       # the in-process multi-device path (no launcher) with two replicas sharing the box's GPU
       timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 20 --warmup 5 > $OUT/bench_multi.json 2> $OUT/bench_multi.err
