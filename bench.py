@@ -378,7 +378,7 @@ def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash
     return roof, stats
 
 
-def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None):
+def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None, prewarm_ms=0.0):
     """A single-GPU BASELINE config beside the headline one: C2 = bunny PRIMARY,
     C5 = bunny FULL, 1920x1080: rate with frames in flight and one frame at a time."""
     W, H = 1920, 1080
@@ -388,7 +388,7 @@ def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None):
     out = {"workload": f"{scene_name}: Stanford bunny (69,451 triangles), {W}x{H} {mode}, eye (0,0,1), 1 light"}
     for fif in (4, 1):
         sc = rt.Scene(mesh, device=device, frames_in_flight=fif)
-        el, st = timed_frames(rt, sc, cam, W, H, m, (0, 1), steps, warmup, lambda: None, lambda: None)
+        el, st = timed_frames(rt, sc, cam, W, H, m, (0, 1), steps, warmup, lambda: None, lambda: None, prewarm_ms)
         key = "" if fif == 4 else "_one_frame_at_a_time"
         out["mrays_per_s" + key] = round(st["primary_rays"] * steps / el / 1e6, 2)
         out["ms_per_frame" + key] = round(el / steps * 1e3, 4)
@@ -407,7 +407,16 @@ def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None):
     return out
 
 
-def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_device):
+def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_device, prewarm_ms=0.0):
+    """W untimed warmup frames, then EXACTLY `steps` timed frames bracketed by barrier + device synchronisation.
+    prewarm_ms: before the warmup frames, frames of the same workload rendered back to back (untimed) for that
+    long, so that the timed frames see the GPU in its loaded state rather than just out of idle (a steady-state
+    rate; the cold start is in profiles/ab/r05_prewarm_ab.txt)."""
+    t_pw = time.perf_counter()
+    while (time.perf_counter() - t_pw) * 1e3 < prewarm_ms:
+        for _ in range(4):
+            sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+        sc.synchronize()
     for _ in range(warmup):
         sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
     sc.synchronize()
@@ -472,6 +481,11 @@ def main():
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="one GPU renders only shard 0 of K (the per-GPU work of a K-GPU C4 run, no collective): "
                          "rehearsal of strong scaling; the line reports that shard's rate")
+    ap.add_argument("--prewarm-ms", type=float, default=50.0,
+                    help="render the workload back to back for this long (untimed) before the warmup steps: the GPU "
+                         "leaves its idle state over tens of milliseconds of load, which 5 warmup frames (~1 ms) do not "
+                         "cover (C3 at 20 steps: 8.4 Grays/s cold, 9.7 after 30-300 ms; profiles/ab/r05_prewarm_ab.txt); "
+                         "0 = off")
     ap.add_argument("--devices", default=None,
                     help="in-process multi-device run (no launcher): the HIP devices of the scene, e.g. 0,1,2,3 "
                          "(default 0..N-1 for --gpus N); repeats allowed to rehearse on one GPU (0,0)")
@@ -570,7 +584,7 @@ def main():
     # the library splits a multi-device scene's frame itself: the caller renders the whole frame
     shard = (0, K) if K else ((0, 1) if devices else (rank, n))
 
-    elapsed, st = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device)
+    elapsed, st = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device, a.prewarm_ms)
     my_rays = st["primary_rays"] * a.steps
     elapsed_max = reduce(elapsed, "MAX")
     total_rays = reduce(float(my_rays), "SUM")
@@ -599,7 +613,7 @@ def main():
         W2, H2 = (3840, 2160) if n == 1 else (1920, 1080)
         cam2 = rt.flycam(W2, H2, 0, 0, 20)
         k2 = max(10, a.steps // 2)
-        el2, st2 = timed_frames(rt, sc, cam2, W2, H2, mode, shard, k2, a.warmup, barrier, sync_device)
+        el2, st2 = timed_frames(rt, sc, cam2, W2, H2, mode, shard, k2, a.warmup, barrier, sync_device, a.prewarm_ms)
         el2 = reduce(el2, "MAX")
         rays2 = reduce(float(st2["primary_rays"] * k2), "SUM")
         extra = {"frame": f"{W2}x{H2}", "workload": "C4 frame on 1 GPU" if n == 1 else f"C3 frame split over {n} GPUs",
@@ -611,7 +625,7 @@ def main():
     side = {}
     if n == 1 and not a.no_side and a.frame is None and a.scene == "soup" and a.mode == "primary" and not K:
         for cn, md in (("c2", "primary"), ("c5", "full")):
-            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local, ident["source_hash"])
+            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local, ident["source_hash"], a.prewarm_ms)
 
     roof = None
     stats = None
@@ -682,7 +696,7 @@ def main():
                                        if n > 1 else "tiles/1 (one GPU, whole frame)"),
                        "launcher": "in-process devices" if devices else ("torchrun" if world > 1 else "none"),
                        "per_gpu": per_gpu if n > 1 else None,
-                       "frames_in_flight": info_fif,
+                       "frames_in_flight": info_fif, "prewarm_ms": a.prewarm_ms,
                        # HIP hardware queues per process: the environment's GPU_MAX_HW_QUEUES (0 = unset, the
                        # runtime's default 4); bench.py leaves it alone
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),

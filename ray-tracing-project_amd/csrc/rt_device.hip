@@ -28,7 +28,8 @@ namespace rt {
 // thread places its contiguous run of waves. Any order is a permutation: every frame renders identical
 // bits.
 constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
-constexpr int kSplitK = 2048;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k)
+constexpr int kSplitK = 1536;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k); round 5
+                               // re-sweep without the spill: 1536 +2.5..6% over 2048 (profiles/ab/r05_c5_split_ab.txt)
 constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
 __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c, int shift) {
   // 4 buckets per octave: exponent and 2 mantissa bits of (float)c; costs of 2^10 .. 2^18 shader cycles
@@ -391,6 +392,7 @@ static void release_slot_stream(int dev, void* st, bool dedicated) {
     g_dedicated_slots[dev]--;
   }
 }
+constexpr int kEventFrames = 128;
 static int init_slots(rt_scene* s, int dev) {
   HIPCHECK(hipSetDevice(dev));
   s->device = dev;
@@ -403,6 +405,13 @@ static int init_slots(rt_scene* s, int dev) {
     s->slots[k].dedicated_queue = dedicated;
   }
   s->stream = s->slots[0].stream;
+  // the timing events of the first kEventFrames frames between two rt_synchronize calls, made here rather than
+  // one frame at a time inside a caller's frame loop
+  for (int k = (int)s->ev_pool.size(); k < 3 * kEventFrames; k++) {
+    hipEvent_t e;
+    HIPCHECK(hipEventCreate(&e));
+    s->ev_pool.push_back(e);
+  }
   return RT_OK;
 }
 
@@ -1133,7 +1142,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       P.cost = slot.d_cost;
     }
   }
-  if (s->ev_used + 3 > s->ev_pool.size()) {
+  if (s->ev_used + 3 > s->ev_pool.size()) {  // (init_slots creates kEventFrames frames' worth up front)
     if (s->ev_pool.size() >= 3 * 2048) { set_error("more than 2048 renders without rt_synchronize"); return RT_ERR_INVALID; }
     for (int k = 0; k < 3; k++) {
       hipEvent_t e;

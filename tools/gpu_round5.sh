@@ -99,7 +99,7 @@ for s in $STEPS; do
       # lone C5 frames: the K costliest waves of the longest-first order as four 16-lane sub-waves (RT_SPLIT_K; product 2048)
       export RTAMD_DEBUG_KNOBS=1
       for rep in 1 2; do
-        for k in 2048 1024 1536 3072; do
+        for k in ${C5K:-2048 1024 1536 3072}; do
           RT_SPLIT_K=$k timeout -k 10 120 python bench.py --scene bunny --mode full --steps 40 --warmup 5 --no-cpu --no-side \
               --no-extra --no-e2e --no-stats --frames-in-flight 1 > $OUT/c5split_${k}_r$rep.json 2> $OUT/c5split_${k}_r$rep.err
           rc=$?; [ $rc -ne 0 ] && { echo "c5split $k rc=$rc"; hard $rc; exit $rc; }
@@ -107,6 +107,28 @@ for s in $STEPS; do
         done
       done
       unset RTAMD_DEBUG_KNOBS ;;
+    steps)
+      # the timed-step count's effect on the C3 line (20 = the driver's), 4 frames in flight
+      for rep in 1 2; do
+        for k in 20 40 100; do
+          timeout -k 10 120 python bench.py --steps $k --warmup 5 --no-cpu --no-side --no-extra --no-e2e --no-stats \
+              > $OUT/steps_${k}_r$rep.json 2> $OUT/steps_${k}_r$rep.err
+          rc=$?; [ $rc -ne 0 ] && { echo "steps $k rc=$rc"; hard $rc; exit $rc; }
+          python3 -c "import json;d=json.loads(open('$OUT/steps_${k}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('steps $k r$rep', d['value'], d['ms_per_step'], c['kernel_ms_per_frame'])"
+        done
+      done ;;
+    prewarm)
+      # GPU state at the timed region's start: frames rendered back to back for P ms before the 5 warmup steps (C3)
+      for rep in 1 2; do
+        for pw in 0 30 100 300; do
+          for k in 20 100; do
+            timeout -k 10 120 python bench.py --steps $k --warmup 5 --prewarm-ms $pw --no-cpu --no-side --no-extra --no-e2e \
+                --no-stats > $OUT/pw_${pw}_${k}_r$rep.json 2> $OUT/pw_${pw}_${k}_r$rep.err
+            rc=$?; [ $rc -ne 0 ] && { echo "prewarm $pw rc=$rc"; hard $rc; exit $rc; }
+            python3 -c "import json;d=json.loads(open('$OUT/pw_${pw}_${k}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('prewarm $pw steps $k r$rep', d['value'], d['ms_per_step'], c['kernel_ms_per_frame'])"
+          done
+        done
+      done ;;
     multi)
       # the in-process multi-device path (no launcher) with two replicas sharing the box's GPU
       timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 20 --warmup 5 > $OUT/bench_multi.json 2> $OUT/bench_multi.err

@@ -47,16 +47,19 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
             out["bench_line_under_trace"] = json.loads(open(bench).read().strip().splitlines()[-1])
         except Exception:
             pass
-    # the same average restricted to the bench's timed launches (dispatch order: warm-up frames first,
-    # then the timed steps; the counting run and the end-to-end frames come after), which is what the
-    # bench line's HIP-event kernel_ms measures
+    # the same average restricted to the bench's timed launches, which is what the bench line's HIP-event
+    # kernel_ms measures. Dispatch order of this kernel (the counting run, the parity frame and the end-to-end
+    # frames use other instantiations or are off under profile.sh): the prewarm frames (round 5), the warm-up
+    # frames, the timed steps, then the 20 isolated frames of bench.isolated_kernel_ms -- so the timed steps
+    # are the K dispatches before the last 20
     trace_csv = os.path.join(prof, "trace", "run_kernel_trace.csv")
     bl = out.get("bench_line_under_trace")
     if bl and os.path.exists(trace_csv):
         rows = [r for r in csv.DictReader(open(trace_csv)) if "::" + kernel in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        w, k = int(bl["warmup"]), int(bl["steps"])
-        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[w:w + k]]
+        k, iso = int(bl["steps"]), 20
+        sel = rows[len(rows) - iso - k:len(rows) - iso] if len(rows) >= iso + k else []
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel]
         if len(d) == k:
             out["avg_kernel_ns_timed_region"] = sum(d) / k
             rl = bl.get("roofline") or {}
