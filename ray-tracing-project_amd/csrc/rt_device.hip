@@ -1056,8 +1056,11 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
                     (fr->max_depth <= 1 || fr->mode == RT_MODE_BOX_COLORS) && !(variant & (1 | 2 | 4 | 32768 | 256 | 2048 | 65536)) &&
                     (variant & 1048576);
   const size_t units = (size_t)grid * (dual ? 2 : 4);  // one-wave blocks of the render kernel
+  // (RT_TIMELINE_SPLIT, diagnostics only: a timeline frame keeps the lone-frame split of its costliest
+  // waves; one record per block, so room for the 3 K extra blocks)
+  const bool timeline_split = (fr->flags & RT_FRAME_TIMELINE) && debug_env("RT_TIMELINE_SPLIT");
   if (fr->flags & RT_FRAME_TIMELINE) {  // one record per one-wave block of the render kernel
-    const size_t waves = units;
+    const size_t waves = timeline_split ? 2 * units : units;
     if (waves > slot.timeline_waves) {
       HIPCHECK(hipStreamSynchronize(st));
       if (slot.d_timeline) (void)hipFree(slot.d_timeline);
@@ -1180,7 +1183,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       const int split_p = split_p_env ? atoi(split_p_env) : kSplitKPrimary;
       // (RT_SPLIT_KP_ANY, A/B only: split lone frames of any scene size)
       const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes || debug_env("RT_SPLIT_KP_ANY");
-      P.split_k = (P.order && small_p && !P.timeline && kTraceWPB == 1)
+      P.split_k = (P.order && small_p && (!P.timeline || timeline_split) && kTraceWPB == 1)
                       ? std::max(0, std::min<int>(split_p, (int)(units / 4))) & ~7 : 0;
       if (P.cost && P.split_k)
         HIPCHECK(hipMemsetAsync(P.cost, 0, units * 4, st));  // sub-waves add / take the max
@@ -1234,7 +1237,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       // depend on the grouping (exact per-lane culling, (t, rank) argmin).
       const char* split_k_env = debug_env("RT_SPLIT_K");
       const int split_env = split_k_env ? atoi(split_k_env) : kSplitK;
-      if (P.order && small && !P.timeline && !stats && kFullWPB == 1 && trav == TRAV_B2_LDS)
+      if (P.order && small && (!P.timeline || timeline_split) && !stats && kFullWPB == 1 && trav == TRAV_B2_LDS)
         P.split_k = std::max(0, std::min<int>(split_env, (int)(units / 4))) & ~7;
       else
         P.split_k = 0;

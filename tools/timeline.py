@@ -7,6 +7,8 @@ analyse (anywhere): python tools/timeline.py analyse OUT.npz
     kernel span from the constant 100 MHz clock, shader clock from s_memtime / s_memrealtime, mean
     resident waves over the span, occupancy over time (ramp / steady / tail), wave-duration spread, and
     what the span would be if every SIMD stayed full (sum of wave time / slots).
+With RTAMD_DEBUG_KNOBS=1 RT_TIMELINE_SPLIT=1 the captured frames keep the lone-frame split of their costliest
+waves (one record per block: blocks 0 .. 4K-1 are 16-lane sub-waves) and the analysis reports them apart.
 """
 import argparse
 import json
@@ -38,12 +40,13 @@ def capture(out, scene, mode, frame, variant=0):
         st = sc.synchronize()
         if flags:
             recs.append((sc.timeline(), st["kernel_ms"]))
+    units = ((W + 15) // 16) * ((H + 15) // 16) * 4
     np.savez_compressed(out, tl=np.stack([r[0] for r in recs]), kernel_ms=np.array([r[1] for r in recs]),
-                        W=W, H=H, mode=mode, scene=scene, identity=json.dumps(rt.build_identity()))
+                        units=units, W=W, H=H, mode=mode, scene=scene, identity=json.dumps(rt.build_identity()))
     print("captured", out, [r[1] for r in recs])
 
 
-def analyse(path):
+def analyse(path, slots_per_simd=8):
     d = np.load(path)
     res = []
     for tl, kms in zip(d["tl"], d["kernel_ms"]):
@@ -64,7 +67,7 @@ def analyse(path):
         for a, b in zip(s, e):
             ia, ib = int(a), int(b)
             occ[ia:ib + 1] += 1
-        slots = 1024 * 8
+        slots = 1024 * slots_per_simd
         wave_us = (e - s)
         ideal = wave_us.sum() / slots
         q = np.percentile(wave_us, [5, 50, 95, 99])
@@ -72,6 +75,23 @@ def analyse(path):
         hw = tl[ok, 6]
         cu = (tl[ok, 7] >> 28) * 1000 + ((hw >> 13) & 3) * 100 + ((hw >> 12) & 1) * 10 + ((hw >> 8) & 15)
         per_cu = np.bincount(np.unique(cu, return_inverse=True)[1], weights=wave_us)
+        # RT_TIMELINE_SPLIT captures: blocks 0 .. 4K-1 are the 16-lane sub-waves of the K costliest waves
+        units = int(d["units"]) if "units" in d.files else None
+        idx = np.nonzero(ok)[0]
+        k_split = (int(ok.sum()) - units) // 3 if units else 0
+        sub = idx < 4 * k_split
+        top = np.argsort(-(e - s))[:12]
+        split_info = {"split_k": k_split} if k_split > 0 else {}
+        if k_split > 0:
+            split_info.update({
+                "sub_wave_us_p50_p95_max": [round(float(x), 1) for x in np.percentile(wave_us[sub], [50, 95, 100])],
+                "whole_wave_us_p50_p95_max": [round(float(x), 1) for x in np.percentile(wave_us[~sub], [50, 95, 100])],
+                "sub_wave_time_share": round(float(wave_us[sub].sum() / wave_us.sum()), 3),
+                "last_sub_wave_end_us": round(float(e[sub].max()), 1),
+                "whole_waves_end_us_p50_p99_max": [round(float(x), 1) for x in np.percentile(e[~sub], [50, 99, 100])],
+            })
+        split_info["longest_blocks"] = [{"block": int(idx[i]), "sub": bool(sub[i]), "start_us": round(float(s[i]), 1),
+                                         "us": round(float(e[i] - s[i]), 1)} for i in top]
         res.append({
             "kernel_ms_hip_events": float(kms), "span_us": round(float(span), 1), "waves": int(ok.sum()),
             "shader_clock_GHz": round(float(clk), 3),
@@ -87,6 +107,7 @@ def analyse(path):
                                                                      round(float(per_cu.max()) / 32, 1)],
             "last_10pct_dispatched_wave_us_mean": round(float(wave_us[int(0.9 * len(wave_us)):].mean()), 1),
             "first_10pct_dispatched_wave_us_mean": round(float(wave_us[: int(0.1 * len(wave_us))].mean()), 1),
+            **split_info,
         })
     for r in res:
         print(json.dumps(r))
@@ -101,8 +122,9 @@ if __name__ == "__main__":
     ap.add_argument("--mode", default="primary")
     ap.add_argument("--frame", default="1920x1080")
     ap.add_argument("--variant", type=int, default=0, help="kernel-variant bits (131072: default dispatch order)")
+    ap.add_argument("--slots", type=int, default=8, help="resident waves per SIMD the kernel is built for (FULL small: 6)")
     a = ap.parse_args()
     if a.cmd == "capture":
         capture(a.path, a.scene, a.mode, a.frame, a.variant)
     else:
-        analyse(a.path)
+        analyse(a.path, a.slots)
