@@ -107,6 +107,18 @@ for s in $STEPS; do
         done
       done
       unset RTAMD_DEBUG_KNOBS ;;
+    c5knob)
+      # lone C5 frames under one debug knob: KNOB=<env name> VALS="<values>" (first value = the product's)
+      export RTAMD_DEBUG_KNOBS=1
+      for rep in 1 2; do
+        for v in $VALS; do
+          env $KNOB=$v timeout -k 10 120 python bench.py --scene bunny --mode full --steps 40 --warmup 5 --no-cpu --no-side \
+              --no-extra --no-e2e --no-stats --frames-in-flight ${FIF:-1} > $OUT/c5knob_${KNOB}_${v}_r$rep.json 2> $OUT/c5knob_${KNOB}_${v}_r$rep.err
+          rc=$?; [ $rc -ne 0 ] && { echo "c5knob $KNOB=$v rc=$rc"; hard $rc; exit $rc; }
+          python3 -c "import json;d=json.loads(open('$OUT/c5knob_${KNOB}_${v}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('c5knob $KNOB=$v r$rep', d['value'], d['ms_per_step'], c['kernel_ms_one_frame_alone'])"
+        done
+      done
+      unset RTAMD_DEBUG_KNOBS ;;
     steps)
       # the timed-step count's effect on the C3 line (20 = the driver's), 4 frames in flight
       for rep in 1 2; do
