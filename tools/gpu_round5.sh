@@ -141,6 +141,9 @@ for s in $STEPS; do
           done
         done
       done ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -3 $OUT/smoke.log; hard $rc; [ $rc -ne 0 ] && exit $rc ;;
     multi)
       # the in-process multi-device path (no launcher) with two replicas sharing the box's GPU
       timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 20 --warmup 5 > $OUT/bench_multi.json 2> $OUT/bench_multi.err
