@@ -1080,14 +1080,34 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     if ((rc = ensure_full(slot, npad))) return rc;
     bind_full(slot, P);
   }
-  // block order: chunked XCD order with runs of 64 blocks by default (measured -4% trace time on C3:
-  // the quarters of a tile and their row neighbours share an XCD's L2); variant bits 512 / 1024 select
-  // runs of 4 / 16 blocks, 1536 the plain dispatch order, 4 one contiguous tile range per XCD
+  // a frame alone on the GPU: no other frame of this scene in flight (the dispatch order below and the
+  // longest-first order depend on it)
+  bool alone = true;
+  for (int k = 0; k < s->n_slots; k++)
+    if (k != slot_id && s->slots[k].last_done && hipEventQuery((hipEvent_t)s->slots[k].last_done) == hipErrorNotReady)
+      alone = false;
+  // block order: chunked XCD order -- block b runs on XCD b % 8, and the XCD's k-th block takes the k-th
+  // position of its runs of C consecutive blocks. With frames in flight C = 64 (measured -4% trace time
+  // on C3 against the plain order: the quarters of a tile and their row neighbours share an XCD's L2;
+  // runs of 32 .. 256 within noise, profiles/ab/r05_xcd_run_ab.txt). A frame alone on the GPU of a scene
+  // whose records exceed the chip's L2 takes one contiguous band of the frame per XCD (C = units / 8), so
+  // that each XCD's L2 holds the part of the scene its band sees: C3 one frame alone +4.5%
+  // (profiles/ab/r05_xcd_bands_ab.txt). Not for L2-resident scenes (bunny one frame alone: PRIMARY -9%,
+  // FULL -6..-12%: nothing to gain in locality, and the XCDs' bands differ in cost), nor with frames in
+  // flight (-1..-3% on C3: every frame's costliest band then sets its XCD's pace). Variant bits
+  // 512 / 1024 select runs of 4 / 16 blocks, 1536 the plain dispatch order, 4 one contiguous tile range
+  // per XCD (256-thread blocks)
   {
     const int sel = (variant >> 9) & 3;
-    P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? 64 : sel == 1 ? 4 : sel == 2 ? 16 : 0);
-    const char* run_env = debug_env("RT_XCD_RUN");  // (A/B only: another run length of the chunked order)
+    const int band = std::max<int>(2, (int)(units / 8));
+    const bool l2_resident = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
+    const bool bands = alone && !l2_resident;
+    P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? (bands ? band : 64) : sel == 1 ? 4 : sel == 2 ? 16 : 0);
+    // (A/B only: another run length of the chunked order for every frame / for lone frames)
+    const char* run_env = debug_env("RT_XCD_RUN");
     if (run_env && atoi(run_env) >= 2) P.xcd_remap = atoi(run_env);
+    const char* alone_env = debug_env("RT_XCD_RUN_ALONE");
+    if (bands && sel == 0 && !(variant & 4) && alone_env && atoi(alone_env) >= 2) P.xcd_remap = atoi(alone_env);
   }
   const int trav = pick_trav(P, variant);
   {
@@ -1113,10 +1133,6 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   // tail of the frame would leave the GPU idle and longest-first fills it (one frame at a time: C3
   // +18%, C5 +28%); with frames in flight the next frame fills the tail and the default order's tile
   // locality is worth more (LPT measured -3..-7% there). Variant 524288 forces it, 131072 disables it.
-  bool alone = true;
-  for (int k = 0; k < s->n_slots; k++)
-    if (k != slot_id && s->slots[k].last_done && hipEventQuery((hipEvent_t)s->slots[k].last_done) == hipErrorNotReady)
-      alone = false;
   const bool lpt = one_wave_kernel && !(variant & 131072) && P.xcd_remap >= 2 && grid > 0 && (alone || (variant & 524288));
   bool lpt_sort = false;
   if (lpt) {
