@@ -1087,27 +1087,24 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     if (k != slot_id && s->slots[k].last_done && hipEventQuery((hipEvent_t)s->slots[k].last_done) == hipErrorNotReady)
       alone = false;
   // block order: chunked XCD order -- block b runs on XCD b % 8, and the XCD's k-th block takes the k-th
-  // position of its runs of C consecutive blocks. With frames in flight C = 64 (measured -4% trace time
-  // on C3 against the plain order: the quarters of a tile and their row neighbours share an XCD's L2;
-  // runs of 32 .. 256 within noise, profiles/ab/r05_xcd_run_ab.txt). A frame alone on the GPU of a scene
-  // whose records exceed the chip's L2 takes one contiguous band of the frame per XCD (C = units / 8), so
-  // that each XCD's L2 holds the part of the scene its band sees: C3 one frame alone +4.5%
-  // (profiles/ab/r05_xcd_bands_ab.txt). Not for L2-resident scenes (bunny one frame alone: PRIMARY -9%,
-  // FULL -6..-12%: nothing to gain in locality, and the XCDs' bands differ in cost), nor with frames in
-  // flight (-1..-3% on C3: every frame's costliest band then sets its XCD's pace). Variant bits
-  // 512 / 1024 select runs of 4 / 16 blocks, 1536 the plain dispatch order, 4 one contiguous tile range
-  // per XCD (256-thread blocks)
+  // position of its runs of C consecutive blocks. Scenes whose records exceed the chip's 32 MiB of L2 take
+  // one contiguous band of the frame per XCD (C = units / 8), so that each XCD's 4 MiB L2 holds the part
+  // of the scene its band sees (L2 hit 0.90 -> 0.94 on C3): a frame alone on the GPU +4.3% on C3, +8.7%
+  // on C4. With frames in flight the XCDs' bands rotate frame by frame (xcd_rot), so that no XCD keeps
+  // the costliest band of every frame: +1.5% on C3 at 100 frames (fixed bands lost 1-3% there); all in
+  // profiles/ab/r05_xcd_bands_ab.txt. L2-resident scenes keep runs of C = 64 (bunny one frame alone with
+  // bands: PRIMARY -9%, FULL -6..-12% -- no locality to gain, and the bands differ in cost; runs of
+  // 32 .. 256 within noise, profiles/ab/r05_xcd_run_ab.txt; 64 against the plain order -4% trace time on
+  // C3 before the bands). Variant bits 512 / 1024 select runs of 4 / 16 blocks, 1536 the plain dispatch
+  // order, 4 one contiguous tile range per XCD (256-thread blocks)
   {
     const int sel = (variant >> 9) & 3;
-    const int band = std::max<int>(2, (int)(units / 8));
     const bool l2_resident = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
-    const bool bands = alone && !l2_resident;
-    P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? (bands ? band : 64) : sel == 1 ? 4 : sel == 2 ? 16 : 0);
-    // (A/B only: another run length of the chunked order for every frame / for lone frames)
-    const char* run_env = debug_env("RT_XCD_RUN");
+    const int run = l2_resident ? 64 : std::max<int>(2, (int)(units / 8));
+    P.xcd_remap = (variant & 4) ? 1 : (sel == 0 ? run : sel == 1 ? 4 : sel == 2 ? 16 : 0);
+    const char* run_env = debug_env("RT_XCD_RUN");  // (A/B only: another run length of the chunked order)
     if (run_env && atoi(run_env) >= 2) P.xcd_remap = atoi(run_env);
-    const char* alone_env = debug_env("RT_XCD_RUN_ALONE");
-    if (bands && sel == 0 && !(variant & 4) && alone_env && atoi(alone_env) >= 2) P.xcd_remap = atoi(alone_env);
+    if (!alone && !l2_resident && P.xcd_remap >= 2) P.xcd_rot = (int32_t)(s->band_rot++ & 7u);
   }
   const int trav = pick_trav(P, variant);
   {

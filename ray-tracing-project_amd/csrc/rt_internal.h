@@ -207,6 +207,7 @@ struct FrameParams {
   // frame
   int32_t W, H, tiles_x, tiles_y;  // tiles = 16x16 pixel blocks (one 256-thread block each)
   int32_t xcd_remap;
+  int32_t xcd_rot;            // chunked XCD order: XCD x takes the runs of XCD x + xcd_rot (mod 8)
   int32_t shard_index, shard_count, n_tiles_shard;
   int32_t super_tile;         // S of shard_tile_xy (1: tile t -> shard t % count)
   int32_t mode, flags;

@@ -1201,7 +1201,7 @@ __device__ __forceinline__ PixelCoord pixel_coord(const FrameParams& P) {
     // over the frame (load balance). The trailing partial group keeps the identity order.
     const int C = P.xcd_remap, G = 8 * C, full = ((int)gridDim.x / G) * G;
     if (bid < full) {
-      const int x = bid & 7, k = bid >> 3;
+      const int x = ((bid & 7) + P.xcd_rot) & 7, k = bid >> 3;
       bid = (k / C) * G + x * C + (k % C);
     }
   }

@@ -213,6 +213,7 @@ struct rt_scene {
   static constexpr int kMaxSlots = 4;
   FrameSlot slots[kMaxSlots];
   int n_slots = 1, next_slot = 0, last_slot = 0;
+  uint32_t band_rot = 0;  // frames in flight: rotation of the XCDs' frame bands (FrameParams::xcd_rot)
   int32_t last_W = 0, last_H = 0, last_flags = 0, last_shard_index = 0, last_shard_count = 1;
   int64_t last_rays = 0, last_total_rays = 0;
   int64_t rays_key[4] = {-1, -1, -1, -1}, rays_of_key = 0;  // primary rays of a frame shape (W, H, shard)
