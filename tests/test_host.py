@@ -20,7 +20,8 @@ def test_header_symbols_exported(rt):
     L = rt.lib()
     for name in sorted(decl):
         assert hasattr(L, name), name
-    assert L.rt_version() == 4
+    want = int(re.search(r"#define RT_API_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert L.rt_version() == want == 4
     ident = rt.build_identity()
     assert ident["matches_tree"], ident
 
@@ -633,3 +634,12 @@ def test_sbvh_build_is_deterministic(rt, tmp_path):
         sc.save(p)
         paths.append(p)
     assert paths[0].read_bytes() == paths[1].read_bytes()
+
+
+def test_graft_entry_library_check(rt):
+    # build()'s final step (the driver's "does it build" check): the library's API version against the header
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("graft_entry", os.path.join(ROOT, "__graft_entry__.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    g.check_library()
