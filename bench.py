@@ -381,6 +381,7 @@ def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash
 def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None, prewarm_ms=0.0):
     """A single-GPU BASELINE config beside the headline one: C2 = bunny PRIMARY,
     C5 = bunny FULL, 1920x1080: rate with frames in flight and one frame at a time."""
+    import torch
     W, H = 1920, 1080
     mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
     m = rt.RT_MODE_FULL if mode == "full" else rt.RT_MODE_PRIMARY
@@ -388,7 +389,8 @@ def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None, prew
     out = {"workload": f"{scene_name}: Stanford bunny (69,451 triangles), {W}x{H} {mode}, eye (0,0,1), 1 light"}
     for fif in (4, 1):
         sc = rt.Scene(mesh, device=device, frames_in_flight=fif)
-        el, st = timed_frames(rt, sc, cam, W, H, m, (0, 1), steps, warmup, lambda: None, lambda: None, prewarm_ms)
+        el, st = timed_frames(rt, sc, cam, W, H, m, (0, 1), steps, warmup, lambda: None,
+                              lambda: torch.cuda.synchronize(device), prewarm_ms)
         key = "" if fif == 4 else "_one_frame_at_a_time"
         out["mrays_per_s" + key] = round(st["primary_rays"] * steps / el / 1e6, 2)
         out["ms_per_frame" + key] = round(el / steps * 1e3, 4)
@@ -425,11 +427,17 @@ def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_de
     t0 = time.perf_counter()
     for _ in range(steps):
         sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
-    st, per = sc.synchronize_devices()
-    st["per_device"] = per
+    # every device of the scene drained (rt_render_async returns once each device's share is queued, so a
+    # device synchronise covers every frame); the frames' event times are read after the clock stops
+    # (rt_synchronize_devices: ~1 us of host time per frame, not part of a frame; profiles/ab/r05_sync_readout_ab.txt)
     sync_device()
     barrier()
     el = time.perf_counter() - t0
+    st, per = sc.synchronize_devices()
+    st["per_device"] = per
+    # the window holds every frame: no frame's own kernel time (HIP events) can exceed it
+    if st["launches"] and el * 1e3 < st["kernel_ms"] / st["launches"]:
+        raise RuntimeError(f"timed window {el * 1e3:.3f} ms shorter than one frame's kernel time: frames not drained")
     # host cost of queueing one frame (rt_render_async through the Python binding), frames not waited on
     t1 = time.perf_counter()
     for _ in range(min(steps, 3)):
@@ -535,8 +543,10 @@ def main():
             dist.barrier()
 
     def sync_device():
+        # every device this process renders on (an in-process multi-device scene spans several)
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            for d in (sorted(set(devices)) if devices else [local]):
+                torch.cuda.synchronize(d)
 
     reduce = make_reducer(dist, dev)
 
