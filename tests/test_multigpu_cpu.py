@@ -161,3 +161,33 @@ def test_bench_refuses_more_gpus_than_visible():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1"],
                        capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_timed_window_must_hold_its_frames():
+    """bench.timed_frames stops its clock after the caller's device synchronise and reads the frames' event times
+    afterwards; a synchronise that drains nothing (the frames still running) must fail, not report the enqueue rate."""
+    import pytest
+
+    class FakeScene:  # frames "take" 1 ms of kernel time each; render_async returns at once
+        def __init__(self):
+            self.n = 0
+
+        def render_async(self, *a, **k):
+            self.n += 1
+
+        def synchronize(self):
+            self.n = 0
+            return {}
+
+        def synchronize_devices(self):
+            n, self.n = self.n, 0
+            return {"kernel_ms": 1.0 * n, "launches": n, "primary_rays": 100}, []
+
+    class FakeRT:
+        DEFAULT_LIGHTS = []
+
+    with pytest.raises(RuntimeError, match="not drained"):
+        bench.timed_frames(FakeRT, FakeScene(), None, 8, 8, 0, (0, 1), 4, 1, lambda: None, lambda: None)
+    el, st = bench.timed_frames(FakeRT, FakeScene(), None, 8, 8, 0, (0, 1), 4, 1, lambda: None,
+                                lambda: __import__("time").sleep(0.01))
+    assert st["launches"] == 4 and el >= 0.01
