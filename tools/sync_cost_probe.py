@@ -1,7 +1,7 @@
 """Where the end of bench.py's timed region goes: C3 (1M soup, 1920x1080 PRIMARY, 4 frames in flight), K frames
 timed as bench.py does (A: rt_synchronize_devices -- wait + per-frame event read-out -- then device synchronise)
 against B (device synchronise only; the event read-out after the clock stops), interleaved reps. Also the host
-cost of the read-out alone (GPU already idle). One JSON line per rep. Usage: python tools/sync_cost_probe.py [K] [reps] [prewarm batch] [early torch init 0/1] [plain|mimic]"""
+cost of the read-out alone (GPU already idle). One JSON line per rep. Usage: python tools/sync_cost_probe.py [K] [reps] [prewarm batch] [early torch init 0/1] [plain|mimic] [prewarm ms]"""
 import importlib.util
 import json
 import os
@@ -34,8 +34,9 @@ def main():
             sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=(0, 1))
 
     mimic = len(sys.argv) > 5 and sys.argv[5] == "mimic"  # prewarm batches end as the timed region does
+    pw = float(sys.argv[6]) / 1e3 if len(sys.argv) > 6 else 0.05  # prewarm seconds
     t = time.perf_counter()
-    while time.perf_counter() - t < 0.05:
+    while time.perf_counter() - t < pw:
         frames(B)
         if mimic:
             sc.synchronize_devices()
@@ -62,7 +63,7 @@ def main():
                 t1 = time.perf_counter()
                 st, _ = sc.synchronize_devices()
                 readout = (time.perf_counter() - t1) * 1e3
-            print(json.dumps({"mimic": mimic, "early_torch_init": early, "B": B, "rep": rep, "form": form, "K": K, "ms_per_frame": round(el / K * 1e3, 4),
+            print(json.dumps({"prewarm_ms": pw * 1e3, "mimic": mimic, "early_torch_init": early, "B": B, "rep": rep, "form": form, "K": K, "ms_per_frame": round(el / K * 1e3, 4),
                               "mrays_s": round(st["primary_rays"] * K / el / 1e6, 1),
                               "enqueue_ms": round((t_q - t0) * 1e3, 3),
                               "readout_ms_idle": None if readout is None else round(readout, 4),
