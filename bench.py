@@ -58,6 +58,7 @@ def frame_for(n_gpus, override):
 
 
 SHARD_SUPER_TILE = 4  # rt_internal.h kShardSuperTile
+MAX_FRAME_SLOTS = 4   # rt_scene.h rt_scene::kMaxSlots: frames a device runs at once (one stream per slot)
 
 
 def shard_tiles(W, H, rank, n):
@@ -297,7 +298,7 @@ DIGESTS = os.path.join(ROOT, "tests", "golden", "fullframe_digests.json")
 SAMPLES = os.path.join(ROOT, "tests", "golden", "fullframe_samples.npz")
 
 
-def frame_parity(rt, sc, W, H, mode, case):
+def frame_parity(rt, sc, W, H, mode, case, cam=None):
     """Parity of the frame this bench times, outside the timed region: one render of the
     same camera with hit records, its per-pixel face ids and t bits hashed (SHA-256) against the oracle's
     committed full-frame digests (tests/golden/fullframe_digests.json, tools/gen_fullframe_digests.py), and
@@ -306,7 +307,9 @@ def frame_parity(rt, sc, W, H, mode, case):
     dig = json.load(open(DIGESTS)).get(case)
     if dig is None or (dig["W"], dig["H"]) != (W, H) or dig["mode"] != ("full" if mode == rt.RT_MODE_FULL else "primary"):
         return {"case": case, "face_t_digest_equal": None, "why": "no committed digest of this frame"}
-    rgb, face, t, _ = sc.render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
+    if cam is None:
+        cam = rt.flycam(W, H, 0, 0, 20)
+    rgb, face, t, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
     sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
     face_ok, t_ok = sha(face) == dig["face_sha256"], sha(t) == dig["t_sha256"]
     out = {"case": case, "pixels": W * H, "face_t_digest_equal": bool(face_ok and t_ok),
@@ -325,6 +328,13 @@ def frame_parity(rt, sc, W, H, mode, case):
     return out
 
 
+def algorithmic_bytes(stats):
+    """The packet algorithm's bytes per launch from a counting run's stats: node / triangle records once per
+    wave, the hit lanes' triangle + shading records, the pixel (module docstring)."""
+    wave_bytes = float(stats["wave_node_bytes"]) + 64.0 * stats["wave_tri_fetches"]
+    return wave_bytes + stats["hits"] * (64 + 48) + 12.0 * max(stats["primary_rays"], 1)
+
+
 def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash, mode_name, latest, split=False,
                 shard=(0, 1), prefer_trace=False):
     """The dominant kernel's packet-byte roofline for one workload (see the module docstring): a counting run
@@ -340,10 +350,7 @@ def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash
     n_tri = stats["tri_tests"] / rays
     hit = stats["hits"] / rays
     kname = ("k_trace_primary" if split else "k_primary_fused") if mode == rt.RT_MODE_PRIMARY else "k_render_full"
-    # the packet algorithm's bytes per launch: node / triangle records once per wave, the hit lanes'
-    # triangle + shading records, the pixel
-    wave_bytes = float(stats["wave_node_bytes"]) + 64.0 * stats["wave_tri_fetches"]
-    alg_bytes = wave_bytes + stats["hits"] * (64 + 48) + 12.0 * rays
+    alg_bytes = algorithmic_bytes(stats)
     prof, prof_src = same_build_profile(W, H, n_faces, mode_name, kname, src_hash, latest)
     trace_ms = (prof.get("avg_kernel_ns_trace") or 0) / 1e6 if prof is not None else 0.0
     hip_ms = kern_ms
@@ -370,6 +377,9 @@ def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "algorithmic_bytes_per_ray": round(alg_bytes / rays, 1),
             "per_step_GBps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            # the same bytes over the throughput interval (frames in flight overlap, so this is the GPU's
+            # sustained rate; `frac` above prices one launch alone)
+            "frac_per_step": round(alg_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "limiter": limiter, "issue": issue,
             # SURVEY 8(d) d3's per-ray demand (every node / triangle a ray visits, as if each ray read
             # its own records): served from SGPRs / L2 / MALL, not HBM -- reported, not priced
@@ -378,7 +388,7 @@ def roofline_of(rt, sc, cam, W, H, mode, kern_ms, ms_per_step, n_faces, src_hash
     return roof, stats
 
 
-def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None, prewarm_ms=0.0):
+def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None, prewarm_ms=0.0, moving=False):
     """A single-GPU BASELINE config beside the headline one: C2 = bunny PRIMARY,
     C5 = bunny FULL, 1920x1080: rate with frames in flight and one frame at a time."""
     import torch
@@ -405,28 +415,105 @@ def side_config(rt, scene_name, mode, steps, warmup, device, src_hash=None, prew
             out["limiter"] = roof["limiter"]
             out["total_mrays_per_s"] = round(s2["total_rays"] * steps / el / 1e6, 2)
             out["parity"] = frame_parity(rt, sc, W, H, m, scene_name)
+            if moving:
+                out["moving_camera"] = moving_camera(
+                    rt, lambda f: rt.Scene(mesh, device=device, frames_in_flight=f), sc, W, H, m, scene_name, steps,
+                    warmup, lambda: torch.cuda.synchronize(device), prewarm_ms)
         del sc
     return out
 
 
-def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_device, prewarm_ms=0.0):
+MOVE_POSE = 37  # the pose (frames along rtamd.CameraPath) whose oracle digest is committed ("<case>-moving")
+
+
+def moving_camera(rt, make_scene, sc4, W, H, mode, case, steps, warmup, sync_device, prewarm_ms):
+    """The workload under the reference's moving camera: every frame a new Flycamera pose
+    (rtamd.CameraPath: WASD held, 0.01 units per axis per frame, flyscene.cpp:116-127, flycamera.hpp:196-202),
+    beside the same measurements with the fixed camera. sc4: the bench's scene (4 frames in flight);
+    make_scene(fif): a new scene of the same workload. Reports the rate with frames in flight, one frame at a time
+    (where the longest-first order comes from an earlier frame's wave costs), the first frame of a fresh scene (no
+    cost map), one frame alone with the default order (no cost map at all, variant 131072), and the roofline of
+    one frame alone under motion."""
+    static = rt.flycam(W, H, 0, 0, 20)
+    out = {"path": "rtamd.CameraPath: Flyscene::simulate with W/S and D/A held (translate(+-0.2, 0, +-0.2) x speed "
+                   "0.05 per frame, turning every 40 / 25 frames), from eye (0,0,1); a new pose every frame"}
+    el, st = timed_frames(rt, sc4, None, W, H, mode, (0, 1), steps, warmup, lambda: None, sync_device, prewarm_ms,
+                          path=rt.CameraPath(W, H))
+    out["mrays_per_s"] = round(st["primary_rays"] * steps / el / 1e6, 2)
+    out["ms_per_frame"] = round(el / steps * 1e3, 4)
+    sc1 = make_scene(1)
+    path = rt.CameraPath(W, H)
+    sc1.render_async(path.next(), rt.DEFAULT_LIGHTS, W, H, mode=mode)  # a fresh scene's first frame: no cost map
+    first = sc1.synchronize()
+    out["first_frame_kernel_ms"] = round(first["trace_kernel_ms"], 4)
+    for key, pth, cam in (("_static", None, static), ("", path, None)):
+        el1, st1 = timed_frames(rt, sc1, cam, W, H, mode, (0, 1), steps, warmup, lambda: None, sync_device, prewarm_ms,
+                                path=pth)
+        out["mrays_per_s_one_frame_at_a_time" + key] = round(st1["primary_rays"] * steps / el1 / 1e6, 2)
+    # one frame alone (HIP events around the render kernel, 20 frames each synchronised before the next)
+    lpt0 = sc1.lpt_stats()
+    iso_m = isolated_kernel_ms(rt, sc1, None, W, H, mode, (0, 1), path=path)
+    lpt1 = sc1.lpt_stats()
+    iso_s = isolated_kernel_ms(rt, sc1, static, W, H, mode, (0, 1))
+    prev = rt.set_variant(131072)  # the default chunked-XCD order: no cost map
+    try:
+        iso_n = isolated_kernel_ms(rt, sc1, None, W, H, mode, (0, 1), path=path)
+    finally:
+        rt.set_variant(prev)
+    out["kernel_ms_isolated"] = round(iso_m[1], 4)
+    out["kernel_ms_isolated_static"] = round(iso_s[1], 4)
+    out["kernel_ms_isolated_no_cost_map"] = round(iso_n[1], 4)
+    out["frame_ms_isolated_incl_sort"] = round(iso_m[0], 4)
+    out["lpt_resorts"] = f"{lpt1['sorts'] - lpt0['sorts']} of {lpt1['frames'] - lpt0['frames']} lone moving frames"
+    # the packet bytes of one frame, averaged over four poses of the path (counting runs), over the kernel time
+    pb = rt.CameraPath(W, H)
+    ab = []
+    for k in range(4):
+        for _ in range(12 if k else 0):
+            pb.next()
+        sc1.render_async(pb.next(), rt.DEFAULT_LIGHTS, W, H, mode=mode, flags=rt.RT_FRAME_STATS)
+        ab.append(algorithmic_bytes(sc1.synchronize()))
+    sc1.render_async(static, rt.DEFAULT_LIGHTS, W, H, mode=mode, flags=rt.RT_FRAME_STATS)
+    ab_s = algorithmic_bytes(sc1.synchronize())
+    ab_m = float(np.mean(ab))
+    out["roofline"] = {"algorithmic_bytes_per_launch": int(ab_m), "unit": "GB/s", "peak": HBM_PEAK_GBPS,
+                       "achieved": round(ab_m / (iso_m[1] * 1e-3) / 1e9, 1),
+                       "frac": round(ab_m / (iso_m[1] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "frac_static": round(ab_s / (iso_s[1] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "frac_no_cost_map": round(ab_m / (iso_n[1] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "kernel_ms_basis": "hip_events (ev_a -> ev_m: the render kernel of a lone frame)"}
+    cp = rt.CameraPath(W, H)
+    cp.take(MOVE_POSE)
+    out["parity"] = frame_parity(rt, sc1, W, H, mode, case + "-moving", cam=cp.camera())
+    del sc1
+    return out
+
+
+def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_device, prewarm_ms=0.0, path=None):
     """W untimed warmup frames, then EXACTLY `steps` timed frames bracketed by barrier + device synchronisation.
     prewarm_ms: before the warmup frames, frames of the same workload rendered back to back (untimed) for that
     long, so that the timed frames see the GPU in its loaded state rather than just out of idle (a steady-state
-    rate; the cold start is in profiles/ab/r05_prewarm_ab.txt)."""
+    rate; the cold start is in profiles/ab/r05_prewarm_ab.txt); their count is returned as st["prewarm_frames"].
+    path (rtamd.CameraPath): every frame -- prewarm, warmup and timed -- takes the path's next pose (the
+    reference's camera moving while a key is held) instead of the fixed `cam`; the timed frames' cameras are
+    made before the clock starts."""
+    nxt = (lambda: path.next()) if path is not None else (lambda: cam)
     t_pw = time.perf_counter()
+    n_pw = 0
     while (time.perf_counter() - t_pw) * 1e3 < prewarm_ms:
         for _ in range(4):
-            sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+            sc.render_async(nxt(), rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+        n_pw += 4
         sc.synchronize()
     for _ in range(warmup):
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+        sc.render_async(nxt(), rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
     sc.synchronize()
+    cams = path.take(steps) if path is not None else [cam] * steps
     barrier()
     sync_device()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    for c in cams:
+        sc.render_async(c, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
     # every device of the scene drained (rt_render_async returns once each device's share is queued, so a
     # device synchronise covers every frame); the frames' event times are read after the clock stops
     # (rt_synchronize_devices: ~1 us of host time per frame, not part of a frame; profiles/ab/r05_sync_readout_ab.txt)
@@ -435,24 +522,35 @@ def timed_frames(rt, sc, cam, W, H, mode, shard, steps, warmup, barrier, sync_de
     el = time.perf_counter() - t0
     st, per = sc.synchronize_devices()
     st["per_device"] = per
-    # the window holds every frame: no frame's own kernel time (HIP events) can exceed it
-    if st["launches"] and el * 1e3 < st["kernel_ms"] / st["launches"]:
-        raise RuntimeError(f"timed window {el * 1e3:.3f} ms shorter than one frame's kernel time: frames not drained")
+    # the window holds every timed frame of every device: a frame slot's stream runs its frames one
+    # after the other, each frame's HIP-event interval (start event -> end event, both recorded on that stream
+    # after the warmup had drained) lies inside the window, so per device the summed frame times cannot exceed
+    # slots x window; and every device rendered every timed frame
+    slots = MAX_FRAME_SLOTS
+    for k, p in enumerate(per or [st]):
+        if p["launches"] != steps:
+            raise RuntimeError(f"device {k}: {p['launches']} frames timed, {steps} queued")
+        if el * 1e3 * slots * 1.001 < p["kernel_ms"]:
+            raise RuntimeError(f"device {k}: frames' kernel time {p['kernel_ms']:.3f} ms exceeds {slots} slots x the "
+                               f"timed window {el * 1e3:.3f} ms: frames not drained")
+    st["prewarm_frames"] = n_pw
     # host cost of queueing one frame (rt_render_async through the Python binding), frames not waited on
+    more = path.take(min(steps, 3)) if path is not None else [cam] * min(steps, 3)
     t1 = time.perf_counter()
-    for _ in range(min(steps, 3)):
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
-    st["enqueue_ms"] = (time.perf_counter() - t1) / min(steps, 3) * 1e3
+    for c in more:
+        sc.render_async(c, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+    st["enqueue_ms"] = (time.perf_counter() - t1) / len(more) * 1e3
     sc.synchronize()
     return el, st
 
 
-def isolated_kernel_ms(rt, sc, cam, W, H, mode, shard, iters=20):
+def isolated_kernel_ms(rt, sc, cam, W, H, mode, shard, iters=20, path=None):
     """The render kernel's launch duration with one frame on the GPU (each frame synchronised before the
-    next is queued): HIP events on the library's stream around each launch, averaged."""
+    next is queued): HIP events on the library's stream around each launch, averaged. path: a new camera pose
+    every frame (rtamd.CameraPath) instead of `cam`."""
     tot, trav = 0.0, 0.0
     for _ in range(iters):
-        sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
+        sc.render_async(path.next() if path is not None else cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=shard)
         st = sc.synchronize()
         tot += st["kernel_ms"]
         trav += st["trace_kernel_ms"]
@@ -494,6 +592,8 @@ def main():
                          "leaves its idle state over tens of milliseconds of load, which 5 warmup frames (~1 ms) do not "
                          "cover (C3 at 20 steps: 8.4 Grays/s cold, 9.7 after 30-300 ms; profiles/ab/r05_prewarm_ab.txt); "
                          "0 = off")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold (no prewarm) rate of the headline frames")
+    ap.add_argument("--no-moving", action="store_true", help="skip the moving-camera sub-lines (C3, C5)")
     ap.add_argument("--devices", default=None,
                     help="in-process multi-device run (no launcher): the HIP devices of the scene, e.g. 0,1,2,3 "
                          "(default 0..N-1 for --gpus N); repeats allowed to rehearse on one GPU (0,0)")
@@ -594,6 +694,16 @@ def main():
     # the library splits a multi-device scene's frame itself: the caller renders the whole frame
     shard = (0, K) if K else ((0, 1) if devices else (rank, n))
 
+    # the cold rate first: the same timed frames with no prewarm, right after the scene setup --
+    # the GPU coming out of idle inside the timed window; then the headline, after a.prewarm_ms of untimed frames
+    cold = None
+    if a.prewarm_ms > 0 and not a.no_cold:
+        el_c, st_c = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device, 0.0)
+        el_c = reduce(el_c, "MAX")
+        cold = {"mrays_per_s": round(reduce(float(st_c["primary_rays"] * a.steps), "SUM") / el_c / 1e6, 2),
+                "ms_per_step": round(el_c / a.steps * 1e3, 4), "steps": a.steps, "warmup": a.warmup, "prewarm_frames": 0,
+                "what": "the same timed frames measured first, right after the scene setup, with no prewarm (the GPU "
+                        "leaving idle inside the window); `value` is the steady state after `prewarm_frames` frames"}
     elapsed, st = timed_frames(rt, sc, cam, W, H, mode, shard, a.steps, a.warmup, barrier, sync_device, a.prewarm_ms)
     my_rays = st["primary_rays"] * a.steps
     elapsed_max = reduce(elapsed, "MAX")
@@ -635,7 +745,18 @@ def main():
     side = {}
     if n == 1 and not a.no_side and a.frame is None and a.scene == "soup" and a.mode == "primary" and not K:
         for cn, md in (("c2", "primary"), ("c5", "full")):
-            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local, ident["source_hash"], a.prewarm_ms)
+            side[cn] = side_config(rt, cn.upper(), md, max(20, a.steps), a.warmup, local, ident["source_hash"], a.prewarm_ms,
+                                   moving=(cn == "c5" and not a.no_moving))
+
+    moving = None
+    if (n == 1 and not a.no_moving and a.frame is None and a.scene == "soup" and a.tris == 1_000_000 and not K
+            and devices is None):
+        def make_scene(fif):
+            mesh, _, _ = rt.soup_mesh(a.tris, 12345)
+            return rt.Scene(mesh, device=local, leaf_size=a.leaf, frames_in_flight=fif, builder=builder,
+                            wide_tree=1 if a.wide else 0, box_builder=0 if a.boxes == "host" else 1)
+        moving = moving_camera(rt, make_scene, sc, W, H, mode, "C3" if a.mode == "primary" else "C3-full", a.steps,
+                               a.warmup, sync_device, a.prewarm_ms)
 
     roof = None
     stats = None
@@ -707,6 +828,9 @@ def main():
                        "launcher": "in-process devices" if devices else ("torchrun" if world > 1 else "none"),
                        "per_gpu": per_gpu if n > 1 else None,
                        "frames_in_flight": info_fif, "prewarm_ms": a.prewarm_ms,
+                       # untimed frames rendered back to back before the warmup (the headline is the steady state
+                       # after them; `cold` below is the same timed frames with none)
+                       "prewarm_frames": st["prewarm_frames"],
                        # HIP hardware queues per process: the environment's GPU_MAX_HW_QUEUES (0 = unset, the
                        # runtime's default 4); bench.py leaves it alone
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
@@ -730,12 +854,18 @@ def main():
             "cpu_baseline": cpu,
             "build": ident,
         }
+        if cold is not None:
+            out["cold"] = cold
+        if moving is not None:
+            out["moving_camera"] = moving
         if extra is not None:
             out["c4_frame" if n == 1 else "c3_frame"] = extra
         out.update(side)
         if headline_parity is not None:
             out["parity"] = headline_parity
-            checked = [headline_parity] + [v["parity"] for v in (side.get("c2"), side.get("c5"), extra) if v and "parity" in v]
+            c5m = (side.get("c5") or {}).get("moving_camera")
+            checked = [headline_parity] + [v["parity"] for v in (side.get("c2"), side.get("c5"), extra, moving, c5m)
+                                           if v and "parity" in v]
             out["parity_all_configs"] = {p["case"]: p["face_t_digest_equal"] for p in checked}
         print(json.dumps(out), flush=True)
     if dist is not None:

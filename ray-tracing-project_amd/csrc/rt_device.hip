@@ -28,6 +28,7 @@ namespace rt {
 // thread places its contiguous run of waves. Any order is a permutation: every frame renders identical
 // bits.
 constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
+constexpr bool kLptMoved = true;  // re-sort after every lone frame whose camera moved since the map's frame
 constexpr int kSplitK = 1536;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k); round 5
                                // re-sweep without the spill: 1536 +2.5..6% over 2048 (profiles/ab/r05_c5_split_ab.txt)
 constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
@@ -583,12 +584,15 @@ void device_release(rt_scene* s) {
   s->d_refbox = nullptr; s->d_mats = nullptr; s->d_stats = nullptr; s->d_pf_check = nullptr;
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
-    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline, f.d_cost, f.d_order};
+    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline};
     for (void* b : fb)
       if (b) (void)hipFree(b);
     release_slot_stream(s->device, f.stream, f.dedicated_queue);
     f = rt_scene::FrameSlot{};
   }
+  if (s->lpt.d_cost) (void)hipFree(s->lpt.d_cost);
+  if (s->lpt.d_order) (void)hipFree(s->lpt.d_order);
+  s->lpt = rt_scene::LptMap{};
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
   s->ev_pool.clear();
   s->ev_used = 0;
@@ -685,6 +689,7 @@ int device_replicate(rt_scene* s) {
     r->opts = s->opts;
     r->opts.n_devices = 0;
     r->opts.device = s->opts.devices[k];
+    r->is_replica = true;
     r->builder_used = s->builder_used;
     r->box_builder_used = s->box_builder_used;
     s->replicas.push_back(std::move(r));
@@ -723,11 +728,15 @@ rt_scene::~rt_scene() { rt::device_release(this); }
 namespace rt {
 
 // RT_MODE_BOX_COLORS: (re)computes the per-face box-colour sums when the colours changed. The scene's
-// streams are drained first (earlier box-colour frames in flight read the table).
+// streams are drained first (earlier box-colour frames in flight read the table). A replica never sets
+// colours itself: render_multi gives the scene its default colours, and with them every replica, before any
+// enqueue worker runs (a replica's worker calling rt_scene_set_box_colors wrote every replica's
+// colour vector while the other workers read theirs).
 static int ensure_face_boxcolor(rt_scene* s) {
   if (s->face_boxcolor_valid) return RT_OK;
   HostScene& hs = s->hs;
   if (s->box_colors.size() != 3 * hs.boxes.size()) {
+    if (s->is_replica) { set_error("device %d: replica without box colours", s->device); return RT_ERR_INVALID; }
     const int rc = rt_scene_set_box_colors(s, nullptr);
     if (rc) return rc;
   }
@@ -931,6 +940,14 @@ extern "C" int rt_debug_counters(rt_scene* s, int64_t n, int64_t* out) {
   return RT_OK;
 }
 
+extern "C" int rt_debug_lpt_stats(const rt_scene* s, int64_t* out3) {
+  if (!s || !out3) { set_error("rt_debug_lpt_stats: null argument"); return RT_ERR_INVALID; }
+  out3[0] = s->lpt.frames;
+  out3[1] = s->lpt.sorts;
+  out3[2] = s->lpt.valid ? 1 : 0;
+  return RT_OK;
+}
+
 extern "C" int rt_debug_env_knobs(int32_t on) {
   set_debug_env(on != 0);
   if (on) {  // RT_KERNEL_VARIANT: the A/B kernel variant of this process (rt_debug_set_variant overrides it)
@@ -1130,32 +1147,45 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   // tail of the frame would leave the GPU idle and longest-first fills it (one frame at a time: C3
   // +18%, C5 +28%); with frames in flight the next frame fills the tail and the default order's tile
   // locality is worth more (LPT measured -3..-7% there). Variant 524288 forces it, 131072 disables it.
+  // (variant 524288, A/B only: also with frames in flight -- then the map is shared by frames that overlap,
+  // a race on the order's values only: any order is a permutation)
   const bool lpt = one_wave_kernel && !(variant & 131072) && P.xcd_remap >= 2 && grid > 0 && (alone || (variant & 524288));
   bool lpt_sort = false;
+  rt_scene::LptMap& lm = s->lpt;
   if (lpt) {
     const size_t waves = units;
-    if (waves > slot.order_waves) {
-      HIPCHECK(hipStreamSynchronize(st));
-      if (slot.d_cost) (void)hipFree(slot.d_cost);
-      if (slot.d_order) (void)hipFree(slot.d_order);
-      slot.d_cost = slot.d_order = nullptr;
-      slot.order_waves = 0;
-      slot.order_valid = false;
-      HIPCHECK(hipMalloc((void**)&slot.d_cost, waves * 4));
-      HIPCHECK(hipMalloc((void**)&slot.d_order, waves * 4));
-      slot.order_waves = waves;
+    if (waves > lm.waves) {
+      for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
+      if (lm.d_cost) (void)hipFree(lm.d_cost);
+      if (lm.d_order) (void)hipFree(lm.d_order);
+      lm.d_cost = lm.d_order = nullptr;
+      lm.waves = 0;
+      lm.valid = false;
+      HIPCHECK(hipMalloc((void**)&lm.d_cost, waves * 4));
+      HIPCHECK(hipMalloc((void**)&lm.d_order, waves * 4));
+      lm.waves = waves;
     }
     const int64_t key[8] = {fr->width, fr->height, si, sc, fr->mode, depth0, P.xcd_remap, (int64_t)waves};
-    const bool same = slot.order_valid && memcmp(key, slot.order_key, sizeof key) == 0;
-    if (same) P.order = slot.d_order;
-    // the order is recomputed from this frame's costs after the frame when it is missing or has served
-    // kLptRefresh frames (the sort costs a few microseconds on the frame's stream; a static or slowly
-    // moving camera keeps its cost map)
-    lpt_sort = !same || ++slot.order_age >= kLptRefresh;
+    const bool same = lm.valid && memcmp(key, lm.key, sizeof key) == 0;
+    if (same) P.order = lm.d_order;
+    // The order is recomputed from this frame's costs after the frame when it is missing, has served
+    // kLptRefresh frames, or -- kLptMoved -- the camera has moved since the frame that recorded it (the
+    // reference's Flycamera moves every frame while a key is held, flyscene.cpp:116-127): a moving camera then
+    // dispatches every lone frame by the previous frame's costs. The sort costs a few microseconds on the frame's
+    // stream. (RT_LPT_REFRESH / RT_LPT_MOVED: A/B knobs, debug environment only.)
+    const char* refresh_env = debug_env("RT_LPT_REFRESH");
+    const char* moved_env = debug_env("RT_LPT_MOVED");
+    const int refresh = refresh_env ? std::max(1, atoi(refresh_env)) : kLptRefresh;
+    const bool key_moved = moved_env ? atoi(moved_env) != 0 : kLptMoved;
+    const bool moved = memcmp(cam->view_matrix, lm.view, sizeof lm.view) != 0;
+    lpt_sort = !same || ++lm.age >= refresh || (key_moved && moved);
+    lm.frames++;
     if (lpt_sort) {
-      memcpy(slot.order_key, key, sizeof key);
-      slot.order_valid = false;  // until this frame's k_order_lpt has been queued
-      P.cost = slot.d_cost;
+      memcpy(lm.key, key, sizeof key);
+      memcpy(lm.view, cam->view_matrix, sizeof lm.view);
+      lm.valid = false;  // until this frame's k_order_lpt has been queued
+      P.cost = lm.d_cost;
+      lm.sorts++;
     }
   }
   if (s->ev_used + 3 > s->ev_pool.size()) {  // (init_slots creates kEventFrames frames' worth up front)
@@ -1269,12 +1299,12 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   } else {
     HIPCHECK(hipEventRecord(ev_m, st));
   }
-  if (lpt_sort) {  // the next frame of this shape on this slot dispatches longest-first
-    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)slot.d_cost, slot.d_order,
+  if (lpt_sort) {  // the scene's next lone frame of this shape dispatches longest-first
+    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)lm.d_cost, lm.d_order,
                        (int)units, P.xcd_remap, (variant & 262144) ? 1 : 0);
     HIPCHECK(hipGetLastError());
-    slot.order_valid = true;
-    slot.order_age = 0;
+    lm.valid = true;
+    lm.age = 0;
   }
   HIPCHECK(hipEventRecord(ev_b, st));
   slot.last_done = ev_b;
@@ -1463,6 +1493,12 @@ static int render_multi(rt_scene* s, const rt_camera* cam, const rt_light* light
     f.shard_index = si + sc * k;
     return f;
   };
+  // the reference's default box colours (setRandomColor draws) reach every replica here, on the caller's
+  // thread, before any worker reads its replica's colours
+  if (fr->mode == RT_MODE_BOX_COLORS && s->box_colors.size() != 3 * s->hs.boxes.size()) {
+    const int rc = rt_scene_set_box_colors(s, nullptr);
+    if (rc) return rc;
+  }
   if (start_workers(s) != RT_OK) {  // (no helper threads: queue every device from this thread)
     for (int k = 0; k < D; k++) {
       const rt_frame f = shard_of(k);

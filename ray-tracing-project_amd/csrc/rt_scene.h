@@ -107,7 +107,7 @@ float scene_static_pad(const HostScene& hs);
 float cert_origin_max(const HostScene& hs);
 uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro);  // kSafeNormalBit | kBoxCertBit of face f
 void set_error(const char* fmt, ...);
-// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_XCD_RUN, RT_LDS_PAD, RT_SAH_TRAV,
+// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_XCD_RUN, RT_LDS_PAD, RT_LPT_REFRESH, RT_LPT_MOVED, RT_SAH_TRAV,
 // RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING): getenv(name) once rt_debug_env_knobs(1) has been called,
 // else nullptr -- the product library's behaviour never depends on the caller's environment otherwise.
 const char* debug_env(const char* name);
@@ -147,6 +147,7 @@ struct rt_scene {
   // and its own frame slots. A frame's tiles are split over the replicas as shards (rt_device.hip
   // render_multi); each replica packs its tiles and copies them into pinned host memory for assembly.
   std::vector<std::unique_ptr<rt_scene>> replicas;
+  bool is_replica = false;  // a replica of another scene (its box colours are set through that scene only)
   // one enqueue worker per replica of replicas (started at the first multi-device frame, stopped before the
   // replicas are released): each replica's launches of a frame are queued by its own host thread
   std::vector<std::shared_ptr<rt::EnqueueWorker>> workers;
@@ -201,15 +202,22 @@ struct rt_scene {
     uint32_t* d_queue = nullptr;  // persistent-threads variant: 8 per-XCD work counters
     uint32_t* d_timeline = nullptr;  // RT_FRAME_TIMELINE records (8 words per wave)
     size_t timeline_waves = 0;
-    // longest-first dispatch order: per-wave costs of this slot's last frame and the order computed
-    // from them for its next frame, valid for frames with the same order_key
+  };
+  // Longest-first dispatch of lone frames (rt_device.hip render_one): the per-wave costs of a recording frame
+  // and the order k_order_lpt computed from them, valid for frames with the same key. One map per scene, not
+  // per frame slot: only a frame alone on the GPU reads or writes it, and such a frame is queued after every
+  // earlier frame (and its sort) has finished, so consecutive lone frames share it whatever slot they take
+  // (round 6: per-slot maps made synchronous frames of a 4-slot scene use a map recorded 4-32 frames earlier).
+  struct LptMap {
     uint32_t* d_cost = nullptr;
     uint32_t* d_order = nullptr;
-    size_t order_waves = 0;
-    int64_t order_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool order_valid = false;  // d_order holds an order for frames of order_key
-    int order_age = 0;         // frames dispatched with that order since it was computed
-  };
+    size_t waves = 0;
+    int64_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool valid = false;     // d_order holds an order for frames of key
+    int age = 0;            // lone frames dispatched with that order since it was computed
+    float view[16] = {0};   // the camera of the frame whose costs made the order
+    int64_t sorts = 0, frames = 0;  // lone frames that re-sorted / dispatched longest-first (rt_debug_lpt_stats)
+  } lpt;
   static constexpr int kMaxSlots = 4;
   FrameSlot slots[kMaxSlots];
   int n_slots = 1, next_slot = 0, last_slot = 0;

@@ -521,7 +521,7 @@ __device__ __forceinline__ PairCoord pair_coord(const FrameParams& P) {
   } else if (P.xcd_remap >= 2) {
     const int C = P.xcd_remap, G = 8 * C, full = ((int)gridDim.x / G) * G;
     if (bid < full) {
-      const int x = bid & 7, k = bid >> 3;
+      const int x = ((bid & 7) + P.xcd_rot) & 7, k = bid >> 3;  // the product's band rotation (pixel_coord)
       bid = (k / C) * G + x * C + (k % C);
     }
   }

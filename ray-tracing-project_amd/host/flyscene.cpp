@@ -60,18 +60,24 @@ void Flyscene::initialize(int width, int height, const std::string& obj_path, in
     o.n_devices = (int32_t)std::min(devices.size(), (size_t)RT_MAX_DEVICES);
     for (int32_t k = 0; k < o.n_devices; k++) o.devices[k] = devices[k];
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  auto done = [&] { setup_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
   // a scene cache skips OBJ parsing and every build
-  if (!cache_path.empty() && rt_scene_load(cache_path.c_str(), &o, &scene_) == RT_OK) return;
+  if (!cache_path.empty() && rt_scene_load(cache_path.c_str(), &o, &scene_) == RT_OK) { done(); return; }
   if (rt_mesh_load_obj(obj_path.c_str(), &mesh_) != RT_OK) {
     fprintf(stderr, "%s\n", rt_last_error());  // reference: "Cannot open", empty mesh
     return;
   }
   rt_mesh_desc d;
   rt_mesh_get_desc(mesh_, &d);
-  if (rt_scene_create(&d, &o, &scene_) != RT_OK) {
+  const auto t1 = std::chrono::steady_clock::now();
+  const int rc = rt_scene_create(&d, &o, &scene_);
+  build_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+  if (rc != RT_OK) {
     fprintf(stderr, "%s\n", rt_last_error());
     return;
   }
+  done();
   if (!cache_path.empty() && rt_scene_save(scene_, cache_path.c_str()) != RT_OK) fprintf(stderr, "%s\n", rt_last_error());
 }
 

@@ -54,6 +54,11 @@ class Flyscene {
   double raytraceScene(int width = 0, int height = 0);
 
   Flycamera* getCamera() { return &flycamera; }
+  // what initialize() built (rt_scene_get_info of the scene) and how long it took (OBJ load + scene setup, or
+  // the cache load), for the CLI's report; false before a successful initialize()
+  bool sceneInfo(rt_scene_info* out) const { return scene_ && rt_scene_get_info(scene_, out) == RT_OK; }
+  double setupSeconds() const { return setup_s_; }   // OBJ load + rt_scene_create (or the cache load)
+  double buildSeconds() const { return build_s_; }   // rt_scene_create alone (boxes, BVH, upload)
 
   // light sources for ray tracing (flyscene.hpp:132)
   std::vector<std::pair<Vec3, Vec3>> lights;
@@ -63,8 +68,12 @@ class Flyscene {
   std::string output = "result.ppm";
   std::vector<float> last_image;         // [H][W][3] float frame (kept only when the 8-bit path was inexact)
   std::string cache_path;                // binary scene cache: loaded if present, written after a build
-  int builder = RT_BUILDER_SAH;          // RT_BUILDER_LBVH_GPU: build the BVH on the GPU
-  int box_builder = RT_BOXES_HOST;       // RT_BOXES_GPU: build the reference box partition on the GPU
+  // acceleration structures: the library default (rt_scene_opts_default), the configuration every bench number
+  // is measured on -- SAH with spatial splits built on the device (RT_BUILDER_SBVH_GPU) and the reference box
+  // partition on the device (RT_BOXES_GPU); RT_BUILDER_SBVH / RT_BOXES_HOST build the same tree and boxes on the
+  // host (seconds for 1M faces), RT_BUILDER_SAH the host binned SAH tree (~5% slower traversal)
+  int builder = RT_BUILDER_SBVH_GPU;
+  int box_builder = RT_BOXES_GPU;
   std::vector<int> devices;              // several GPUs render every frame (rt_scene_opts.devices); empty: the
                                          // `device` of initialize(); {RT_DEVICES_ALL}: every visible GPU
 
@@ -72,6 +81,7 @@ class Flyscene {
   Flycamera flycamera;
   rt_mesh* mesh_ = nullptr;
   rt_scene* scene_ = nullptr;
+  double setup_s_ = 0.0, build_s_ = 0.0;
 };
 
 }  // namespace fly

@@ -33,7 +33,7 @@ EXPORTS = [
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
     "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
     "rt_debug_record_layout", "rt_debug_scene_flags", "rt_debug_env_knobs", "rt_debug_tree_cost",
-    "rt_synchronize_devices",
+    "rt_synchronize_devices", "rt_debug_lpt_stats",
 ]
 RT_MAX_DEVICES = 16
 RT_DEVICES_ALL = -1
@@ -154,6 +154,8 @@ def lib():
             L.rt_debug_env_knobs(1)
         L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_debug_counters.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
+        if hasattr(L, "rt_debug_lpt_stats"):  # (API 4 libraries of round 5, loaded for A/B, lack it)
+            L.rt_debug_lpt_stats.argtypes = [vp, C.POINTER(C.c_int64)]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
         L.rt_frame_download_rgb8.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
@@ -369,6 +371,12 @@ class Scene:
         check(lib().rt_debug_scene_flags(self.h, _p(out), C.byref(ro), _p(ff)))
         return ff, float(ro.value)
 
+    def lpt_stats(self):
+        """Longest-first dispatch of lone frames (rt_debug_lpt_stats): {frames, sorts, valid}."""
+        out = (C.c_int64 * 3)()
+        check(lib().rt_debug_lpt_stats(self.h, out))
+        return {"frames": int(out[0]), "sorts": int(out[1]), "valid": bool(out[2])}
+
     def counters(self, n=16):
         """Raw counters of the last RT_FRAME_STATS frame (rt_debug_counters): int64 [n]."""
         out = (C.c_int64 * n)()
@@ -546,6 +554,69 @@ def flycam(W, H, dx=0.0, dy=0.0, dz=0.0):
     c = Camera()
     lib().rt_camera_flycam(W, H, dx, dy, dz, C.byref(c))
     return c
+
+
+FLYCAM_SPEED = np.float32(0.05)  # Tucano::Flycamera::speed (flycamera.hpp:107)
+WASD_STEP = 0.2                  # Flyscene::simulate: a held key moves 0.2 per frame (flyscene.cpp:116-127)
+
+
+def flycam_tv(W, H, tv):
+    """The Flycamera of Flyscene::initialize (fovy 60, aspect W/H, viewport) whose translation_vector is tv
+    (float32[3]), after updateViewMatrix at zero rotation (flycamera.hpp:166-191): view = T(0,0,-2) * T(tv), i.e.
+    the view translation (0 + tv.x, 0 + tv.y, -2 + tv.z) in float -- what rt_camera_flycam computes for one
+    translate() from the default pose (tests/test_host.py holds the two equal)."""
+    tv = np.asarray(tv, np.float32)
+    c = Camera()
+    m = np.eye(4, dtype=np.float32).reshape(-1)  # column-major; identity linear part
+    m[12] = np.float32(0.0) + tv[0]
+    m[13] = np.float32(0.0) + tv[1]
+    m[14] = np.float32(-2.0) + tv[2]
+    for k in range(16):
+        c.view_matrix[k] = float(m[k])
+    c.viewport[:] = [0.0, 0.0, float(W), float(H)]
+    c.fovy = 60.0
+    c.aspect_ratio = float(np.float32(W) / np.float32(H))
+    return c
+
+
+class CameraPath:
+    """The camera of the reference's interactive loop (main.cpp:123-130: paintGL, then simulate) with keys held:
+    every frame Flyscene::simulate calls flycamera.translate(dx, dy, dz) with +-0.2 per held key
+    (flyscene.cpp:116-127), and Flycamera::translate adds yaw * (-dx, -dy, dz) * speed to its translation vector
+    in float (flycamera.hpp:196-202; yaw = identity at rotation_Y_axis 0): 0.01 scene units per axis per frame.
+    The path holds W (forward) and D (strafe) and turns each round -- W <-> S every `period_z` frames, D <-> A every
+    `period_x` -- so the pose stays within 0.4 x 0.25 units of the start while it changes every frame. Starts
+    from the bench's pose translate(dx0, dy0, dz0) (eye (0, 0, 1) for dz0 = 20)."""
+
+    def __init__(self, W, H, dx0=0.0, dy0=0.0, dz0=20.0, period_z=40, period_x=25):
+        self.W, self.H = W, H
+        self.i = 0
+        self.pz, self.px = period_z, period_x
+        self.tv = np.zeros(3, np.float32)
+        self._move(dx0, dy0, dz0)
+
+    def _move(self, dx, dy, dz):
+        v = np.array([-dx, -dy, dz], np.float32)          # yaw * Vector3f(-dx, -dy, dz): identity rotation
+        self.tv = (self.tv + v * FLYCAM_SPEED).astype(np.float32)
+
+    def keys(self, i):
+        """(dx, dy, dz) of frame i's simulate(): D / A and W / S alternating."""
+        dz = WASD_STEP if (i // self.pz) % 2 == 0 else -WASD_STEP
+        dx = WASD_STEP if (i // self.px) % 2 == 0 else -WASD_STEP
+        return dx, 0.0, dz
+
+    def camera(self):
+        return flycam_tv(self.W, self.H, self.tv)
+
+    def next(self):
+        """The camera for the next frame: the current pose is rendered, then simulate() moves it."""
+        c = self.camera()
+        self._move(*self.keys(self.i))
+        self.i += 1
+        return c
+
+    def take(self, n):
+        return [self.next() for _ in range(n)]
 
 
 def generate_soup(n_tris, seed=12345):

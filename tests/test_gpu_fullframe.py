@@ -251,3 +251,36 @@ def test_wide_tree_frames_match_oracle_digests(rt, scenes, case, builder):
         st = w.render(rt.flycam(d["W"], d["H"], 0, 0, 20), rt.DEFAULT_LIGHTS, d["W"], d["H"], flags=rt.RT_FRAME_STATS)[-1]
         assert st["wave_node_bytes"] > 64 * 0 and st["wave_node_fetches"] > 0
         assert st["wave_node_bytes"] > 64 * st["wave_node_fetches"]  # 128-B wide records dominate
+
+
+MOVE_POSE = 37  # bench.py / tools/gen_fullframe_digests.py MOVE_POSE
+
+
+@pytest.mark.parametrize("case", ["C3-moving", "C5-moving"])
+@pytest.mark.parametrize("fif", [1, 4])
+def test_moving_camera_frames_match_oracle_digests(rt, scenes, case, fif):
+    """The reference's moving camera: a scene renders frames 0 .. MOVE_POSE - 1 of the camera
+    path one at a time (rtamd.CameraPath: WASD held, flyscene.cpp:116-127), so every frame is dispatched
+    longest-first by a cost map an earlier pose recorded, re-sorted as the camera moves; the frame at pose
+    MOVE_POSE then equals the oracle's committed digests of that pose (face ids and t bits of every pixel) -- the
+    dispatch order, stale or fresh, never changes a pixel. fif 4: frames of a 4-slot scene rendered synchronously
+    (rt_render) share one scene-level map."""
+    d = DIG[case]
+    W, H, mode = d["W"], d["H"], d["mode"]
+    mesh = scenes["soup_mesh" if d["scene"] == "soup" else "bunny_mesh"]
+    sc = rt.Scene(mesh, frames_in_flight=fif)
+    m = rt.RT_MODE_FULL if mode == "full" else rt.RT_MODE_PRIMARY
+    p = rt.CameraPath(W, H)
+    for _ in range(MOVE_POSE):
+        sc.render(p.next(), rt.DEFAULT_LIGHTS, W, H, mode=m)
+    lpt = sc.lpt_stats()
+    assert lpt["frames"] >= MOVE_POSE - 1 and lpt["sorts"] >= MOVE_POSE - 1 and lpt["valid"], lpt
+    rgb, face, t, _ = sc.render(p.camera(), rt.DEFAULT_LIGHTS, W, H, mode=m, want_hits=True)
+    assert sha(face) == d["face_sha256"] and sha(t) == d["t_sha256"], case
+    assert int((np.asarray(face) >= 0).sum()) == d["hits"]
+    smp = np.load(os.path.join(GOLDEN, "fullframe_samples.npz"))
+    idx = smp[case + "_idx"]
+    err = np.abs(np.asarray(rgb, np.float64).reshape(-1, 3)[idx] - smp[case + "_rgb"].astype(np.float64))
+    assert float(np.nanmax(err)) < TOL
+    PARITY_REPORT.append(f"{case} (pose {MOVE_POSE} of the moving camera, {fif} slot(s), {lpt['sorts']} re-sorts): "
+                         f"face/t digests of all {W * H} pixels equal the oracle's")

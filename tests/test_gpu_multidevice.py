@@ -92,6 +92,35 @@ def test_c5_three_devices_equal_one_device_and_oracle(rt, bunny):
     # test_gpu_fullframe.py)
 
 
+@pytest.mark.parametrize("case", ["C4", "C5"])
+def test_distinct_devices_equal_one_device_and_oracle(rt, soup, bunny, case):
+    """The same frames on DISTINCT GPUs (devices 0..n-1 of the node: peer access, hipMemcpyPeerAsync over xGMI,
+    one enqueue worker per GPU, assembly across devices). Skipped on a one-GPU box: there the
+    in-process multi-device path is verified only with replicas sharing device 0 (the tests above)."""
+    n = rt.device_count()
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: distinct-device replication needs 2 or more")
+    d = DIG[case]
+    W, H = d["W"], d["H"]
+    mode = "primary" if case == "C4" else "full"
+    src = soup if case == "C4" else bunny
+    devs = list(range(min(n, rt.RT_MAX_DEVICES)))
+    sc = rt.Scene(src["mesh"], devices=devs)
+    assert sc.info()["n_devices"] == len(devs)
+    one = frame(rt, src["one"], W, H, mode)
+    many = frame(rt, sc, W, H, mode)
+    for a, b in zip(one[:3], many[:3]):
+        assert np.asarray(a).tobytes() == np.asarray(b).tobytes()
+    assert sha(many[1]) == d["face_sha256"] and sha(many[2]) == d["t_sha256"]
+    img8 = []
+    for s in (src["one"], sc):
+        s.render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H,
+                 mode=rt.RT_MODE_FULL if mode == "full" else rt.RT_MODE_PRIMARY)
+        img8.append(s.download_rgb8(W, H)[0])
+    assert img8[0].tobytes() == img8[1].tobytes()
+    PARITY_REPORT.append(f"{case} on distinct devices {devs}: assembled frame == 1 device bit for bit; digests = oracle's")
+
+
 def test_per_device_stats_cover_the_frame(rt, soup):
     """rt_synchronize_devices: one entry per device, their rays add up to the frame, the totals' kernel time
     is the slowest device's."""
@@ -179,6 +208,24 @@ def test_box_colour_frames_on_multi_device_scene(rt, bunny):
         out.append(rgb)
         sc.set_box_colors(None)
     assert out[0].tobytes() == out[1].tobytes()
+
+
+def test_default_box_colours_on_fresh_multi_device_scene(rt, bunny):
+    """RT_MODE_BOX_COLORS on a fresh {0, 0, 0} scene whose colours were never set (the reference's default
+    setRandomColor path): the colours are drawn once on the caller's thread before any replica's
+    worker runs; the frame equals a fresh one-device scene's bit for bit, twice in a row."""
+    W, H = 640, 360
+    cam = rt.flycam(W, H, 0, 0, 20)
+    out = []
+    for devs in (None, [0, 0, 0]):
+        sc = rt.Scene(bunny["mesh"], devices=devs)
+        a, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_BOX_COLORS)
+        b, _ = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_BOX_COLORS)
+        assert a.tobytes() == b.tobytes()
+        out.append(a)
+        del sc
+    assert out[0].tobytes() == out[1].tobytes()
+    assert np.asarray(out[0]).any()
 
 
 def test_scene_cache_load_on_multi_device(rt, bunny):

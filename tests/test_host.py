@@ -92,6 +92,26 @@ def test_camera_matches_oracle(rt, orc, dxyz, WH):
     assert a.fovy == b.fovy and a.aspect_ratio == b.aspect
 
 
+@pytest.mark.parametrize("dxyz", [(0, 0, 0), (0, 0, 20), (3, -2, 7), (-0.2, 0.0, 0.2)])
+def test_camera_path_matches_flycam(rt, dxyz):
+    """The moving-camera path (rtamd.CameraPath: Flyscene::simulate's WASD translate per frame, float
+    accumulation of Flycamera::translation_vector) starts at exactly the pose rt_camera_flycam gives for the same
+    translate, and every step moves the pose by the reference's 0.2 x speed 0.05 per held key."""
+    W, H = 1920, 1080
+    p = rt.CameraPath(W, H, *dxyz)
+    a, b = p.camera(), rt.flycam(W, H, *dxyz)
+    assert list(a.view_matrix) == list(b.view_matrix)
+    assert list(a.viewport) == list(b.viewport) and a.fovy == b.fovy and a.aspect_ratio == b.aspect_ratio
+    cams = p.take(120)
+    t = np.array([[c.view_matrix[12], c.view_matrix[13], c.view_matrix[14]] for c in cams], np.float64)
+    step = np.abs(np.diff(t, axis=0))
+    assert np.allclose(step[:, 0], 0.01, atol=1e-6) and np.allclose(step[:, 2], 0.01, atol=1e-6)
+    assert (step[:, 1] == 0).all()
+    # the path turns round (W <-> S every 40 frames, D <-> A every 25): bounded, and every frame a new pose
+    assert np.ptp(t[:, 2]) <= 0.41 and np.ptp(t[:, 0]) <= 0.26
+    assert len({tuple(x) for x in t}) > 100
+
+
 @pytest.mark.parametrize("sec", read_kat(), ids=lambda s: f"op{s[0]}")
 def test_host_math_matches_eigen(rt, sec):
     op, n, il, ol, inp, exp = sec

@@ -188,6 +188,11 @@ def test_timed_window_must_hold_its_frames():
 
     with pytest.raises(RuntimeError, match="not drained"):
         bench.timed_frames(FakeRT, FakeScene(), None, 8, 8, 0, (0, 1), 4, 1, lambda: None, lambda: None)
+    # a window that could hold the frames only if more than the library's 4 frame slots ran at once (ADVICE r5:
+    # the bound is the summed frame time / slots, not one frame's time)
+    with pytest.raises(RuntimeError, match="not drained"):
+        bench.timed_frames(FakeRT, FakeScene(), None, 8, 8, 0, (0, 1), 8, 1, lambda: None,
+                           lambda: __import__("time").sleep(0.0015))
     el, st = bench.timed_frames(FakeRT, FakeScene(), None, 8, 8, 0, (0, 1), 4, 1, lambda: None,
                                 lambda: __import__("time").sleep(0.01))
-    assert st["launches"] == 4 and el >= 0.01
+    assert st["launches"] == 4 and el >= 0.01 and st["prewarm_frames"] == 0

@@ -37,7 +37,32 @@ CASES = {
     "C3-full": ("soup", 1920, 1080, "full", None),
     "C4": ("soup", 3840, 2160, "primary", None),
     "bunny-depth3": ("bunny", 1920, 1080, "full", 3),
+    # the moving camera (round 6): the pose MOVE_POSE frames along rtamd.CameraPath (the
+    # reference's WASD translate per frame, flyscene.cpp:116-127), the pose bench.py's moving_camera checks
+    "C3-moving": ("soup", 1920, 1080, "primary", None),
+    "C5-moving": ("bunny", 1920, 1080, "full", None),
 }
+MOVE_POSE = 37  # bench.py MOVE_POSE
+
+
+def case_camera(key, W, H):
+    """The oracle camera of a case: Flycamera translate(0, 0, 20), or for *-moving the path pose, built by the
+    product's host-side path helper (pure float32 arithmetic, no device) and copied into the oracle's struct."""
+    if not key.endswith("-moving"):
+        return O.flycam(W, H, 0, 0, 20), None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rtamd", os.path.join(ROOT, "ray-tracing-project_amd", "rtamd.py"))
+    rt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rt)
+    p = rt.CameraPath(W, H)
+    p.take(MOVE_POSE)
+    c = p.camera()
+    oc = O.Camera()
+    for k in range(16):
+        oc.view[k] = c.view_matrix[k]
+    oc.viewport[:] = list(c.viewport)
+    oc.fovy, oc.aspect = c.fovy, c.aspect_ratio
+    return oc, [c.view_matrix[12], c.view_matrix[13], c.view_matrix[14]]
 
 
 def digest(a):
@@ -60,9 +85,8 @@ def oracle_scene(name):
     return O.Scene(O.Mesh.load_obj(os.path.join(ROOT, "scenes", name + ".obj")))
 
 
-def render_case(sc, W, H, mode, max_depth, threads):
-    return sc.render(O.flycam(W, H, 0, 0, 20), O.DEFAULT_LIGHTS, W, H, full=(mode == "full"), threads=threads,
-                     max_depth=max_depth)
+def render_case(sc, cam, W, H, mode, max_depth, threads):
+    return sc.render(cam, O.DEFAULT_LIGHTS, W, H, full=(mode == "full"), threads=threads, max_depth=max_depth)
 
 
 def main():
@@ -82,11 +106,14 @@ def main():
         if scene not in scenes:
             scenes[scene] = oracle_scene(scene)
         t0 = time.time()
-        rgb, face, t = render_case(scenes[scene], W, H, mode, depth, a.threads)
+        cam, view_t = case_camera(key, W, H)
+        rgb, face, t = render_case(scenes[scene], cam, W, H, mode, depth, a.threads)
         dt = time.time() - t0
         rec = frame_record(rgb, face, t)
         rec.update({"scene": scene, "W": W, "H": H, "mode": mode, "max_depth": depth, "eye_dz": 20,
                     "oracle_s": round(dt, 1), "threads": a.threads})
+        if view_t is not None:
+            rec.update({"camera_path_pose": MOVE_POSE, "view_translation": view_t})
         out[key] = rec
         idx = np.arange(0, W * H, SAMPLE_STRIDE)
         samples[key + "_idx"] = idx.astype(np.int32)

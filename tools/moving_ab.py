@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Lone frames under the reference's moving camera: one frame at a time (each frame
+synchronised before the next is queued, as rt_render does), a static camera against rtamd.CameraPath (WASD held,
+flyscene.cpp:116-127), on a 1-slot and a 4-slot scene, for the longest-first dispatch policies of this library
+(RT_LPT_MOVED / RT_LPT_REFRESH debug knobs) or another build of it (RTAMD_LIB, e.g. the round-5 library whose
+cost maps were per frame slot). One JSON line per measurement.
+
+Usage: RTAMD_DEBUG_KNOBS=1 python tools/moving_ab.py <soup|bunny> <primary|full> <policy> [frames] [reps]
+  policy: lib (the library as built), moved0 / moved1 (RT_LPT_MOVED), r1 (RT_LPT_REFRESH=1), nolpt (variant 131072)
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+scene, mode, policy = sys.argv[1], sys.argv[2], sys.argv[3]
+frames = int(sys.argv[4]) if len(sys.argv) > 4 else 60
+reps = int(sys.argv[5]) if len(sys.argv) > 5 else 2
+env = {"moved0": {"RT_LPT_MOVED": "0"}, "moved1": {"RT_LPT_MOVED": "1"}, "r1": {"RT_LPT_REFRESH": "1"}}.get(policy, {})
+os.environ.update(env)
+rt = bench.load_rtamd()
+import torch  # noqa: E402
+
+W, H = 1920, 1080
+if scene == "soup":
+    mesh, _, _ = rt.soup_mesh(1_000_000, 12345)
+else:
+    mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
+m = rt.RT_MODE_FULL if mode == "full" else rt.RT_MODE_PRIMARY
+if policy == "nolpt":
+    rt.set_variant(131072)
+lib = os.path.basename(os.environ.get("RTAMD_LIB", "librtamd.so"))
+for fif in (1, 4):
+    sc = rt.Scene(mesh, frames_in_flight=fif)
+    static = rt.flycam(W, H, 0, 0, 20)
+    for _ in range(40):  # warm the GPU and the maps
+        sc.render_async(static, rt.DEFAULT_LIGHTS, W, H, mode=m)
+        sc.synchronize()
+    for rep in range(reps):
+        for cam_kind in ("static", "moving"):
+            path = rt.CameraPath(W, H) if cam_kind == "moving" else None
+            for _ in range(10):  # the path's first poses (untimed)
+                sc.render_async(path.next() if path else static, rt.DEFAULT_LIGHTS, W, H, mode=m)
+                sc.synchronize()
+            cams = path.take(frames) if path else [static] * frames
+            k_ms = tr_ms = 0.0
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for c in cams:
+                sc.render_async(c, rt.DEFAULT_LIGHTS, W, H, mode=m)
+                st = sc.synchronize()
+                k_ms += st["kernel_ms"]
+                tr_ms += st["trace_kernel_ms"]
+            el = time.perf_counter() - t0
+            rec = {"lib": lib, "policy": policy, "scene": scene, "mode": mode, "fif": fif, "rep": rep, "camera": cam_kind,
+                   "frames": frames, "mrays_per_s_one_at_a_time": round(W * H * frames / el / 1e6, 1),
+                   "frame_ms_wall": round(el / frames * 1e3, 4), "kernel_ms": round(tr_ms / frames, 4),
+                   "frame_ms_events": round(k_ms / frames, 4)}
+            if hasattr(rt.lib(), "rt_debug_lpt_stats"):
+                rec["lpt"] = sc.lpt_stats()
+            print(json.dumps(rec), flush=True)
+    del sc
