@@ -169,14 +169,15 @@ def e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist, iters=5):
     gathered = torch.empty(n * slice_b, dtype=torch.uint8, device="cuda" if on_gpu else "cpu")
     frame = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    ts = []
+    ts, ta = [], []
     for _ in range(iters + 1):
         if dist is not None:
             dist.barrier()
         t = time.perf_counter()
         sc.render_async(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, shard=(rank, n))
         sc.synchronize()
-        if n == 1 or dist is None:  # (an in-process multi-device scene assembles its frame on the host)
+        t_a = time.perf_counter()
+        if n == 1 or dist is None:  # (an in-process multi-device scene assembles its frame itself: rt_frame_download_rgb8)
             host, _ = sc.download_rgb8(W, H)
         else:
             sc.pack_shard_rgb8(slc.data_ptr())
@@ -190,7 +191,9 @@ def e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist, iters=5):
                 rt.unpack_shards_rgb8(src.data_ptr(), n, W, H, frame.data_ptr(), torch.cuda.current_device())
                 host = frame.cpu()
         ts.append((time.perf_counter() - t) * 1e3)
-    return sorted(ts[1:])[len(ts[1:]) // 2]
+        ta.append((time.perf_counter() - t_a) * 1e3)
+    med = lambda v: sorted(v[1:])[len(v[1:]) // 2]
+    return med(ts), med(ta)
 
 
 def backend_is_nccl(dist):
@@ -779,9 +782,10 @@ def main():
         sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=mode, want_hits=True)
         gpu_frame = sc.download(W, H, want_hits=True)
 
-    e2e = None
+    e2e = asm_ms = None
     if not a.no_e2e and torch.cuda.is_available():
-        e2e = reduce(e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist), "MAX")
+        e2e, asm_ms = e2e_frame_ms(rt, sc, cam, W, H, mode, rank, n, dist)
+        e2e, asm_ms = reduce(e2e, "MAX"), reduce(asm_ms, "MAX")
 
     cpu = None
     if rank == 0 and n == 1 and not a.no_cpu:
@@ -799,6 +803,9 @@ def main():
         if e2e is not None:
             # one frame end to end: render + 8-bit frame assembled on rank 0 (RCCL all-gather for N>1) + D2H
             more["e2e_frame_ms"] = round(e2e, 3)
+            # of it, after the render: the 8-bit frame assembled and on the host (one GPU: conversion + copy; an
+            # in-process multi-device scene: its device-side assembly; torchrun: pack, all-gather, unpack, copy)
+            more["assembly_ms"] = round(asm_ms, 3)
         if stats is not None:
             more["rays_per_frame_total"] = stats["total_rays"]  # primary + shadow + reflection (FULL)
             # (a rank's own rays times the ranks; a multi-device scene's stats already cover every device)

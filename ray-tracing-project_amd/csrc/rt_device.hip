@@ -29,6 +29,7 @@ namespace rt {
 // bits.
 constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
 constexpr bool kLptMoved = true;  // re-sort after every lone frame whose camera moved since the map's frame
+constexpr int kLptDilate = 1;     // a moving camera's map: each wave's cost = the max over (2r+1)^2 waves around it
 constexpr int kSplitK = 1536;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k); round 5
                                // re-sweep without the spill: 1536 +2.5..6% over 2048 (profiles/ab/r05_c5_split_ab.txt)
 constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
@@ -84,6 +85,31 @@ __global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost,
     const uint32_t rr = mine[lpt_bucket(cost[j], shift)]++;
     order[8 * rr + x] = (uint32_t)j;
   }
+}
+
+// A moving camera's cost map (the reference's Flycamera moves every frame a key is held): between two frames the
+// image shifts by about a wave (C5's bunny: ~9 pixels per 0.01-unit step), so the waves an earlier frame found
+// costly sit next to the ones that will be. Before the sort, each wave takes the maximum recorded cost over the
+// (2r+1) x (2r+1) waves around it in the frame's wave grid (8x8-pixel waves; whole frames only: logical wave
+// j = 4 * tile + quarter, tile t = ty * tiles_x + tx), so the longest-first order and the split of the costliest
+// waves cover where the costly region moves to.
+__global__ __launch_bounds__(256) void k_cost_dilate(const uint32_t* cost, uint32_t* out, int tiles_x, int tiles_y, int n, int r) {
+  const int j = (int)(blockIdx.x * 256u + threadIdx.x);
+  if (j >= n) return;
+  const int t = j >> 2, q = j & 3;
+  const int wx = (t % tiles_x) * 2 + (q & 1), wy = (t / tiles_x) * 2 + (q >> 1), gw = 2 * tiles_x, gh = 2 * tiles_y;
+  uint32_t m = 0;
+  for (int dy = -r; dy <= r; dy++) {
+    const int y = wy + dy;
+    if (y < 0 || y >= gh) continue;
+    for (int dx = -r; dx <= r; dx++) {
+      const int x = wx + dx;
+      if (x < 0 || x >= gw) continue;
+      const int k = 4 * ((y >> 1) * tiles_x + (x >> 1)) + (y & 1) * 2 + (x & 1);
+      if (k < n) m = max(m, cost[k]);
+    }
+  }
+  out[j] = m;
 }
 
 // RT_MODE_BOX_COLORS, once per colour set: for every face id, color += box->color over the reference
@@ -199,6 +225,39 @@ __global__ __launch_bounds__(256) void k_unpack_shards(const uint8_t* packed, ui
   frame[3 * p + 0] = src[0];
   frame[3 * p + 1] = src[1];
   frame[3 * p + 2] = src[2];
+}
+
+// Device-side assembly of a multi-device scene's frame (assemble_device): block (L, k) places tile slot L of replica
+// k's packed slice (k_pack_tiles32 / k_pack_shard layout: 256 pixels of E bytes per tile) into the frame on device 0
+struct UnpackArgs {
+  int32_t n_rep, W, H, tiles_x, E;
+  int32_t si[RT_MAX_DEVICES], sc[RT_MAX_DEVICES], S[RT_MAX_DEVICES], n_tiles[RT_MAX_DEVICES];
+  uint64_t off[RT_MAX_DEVICES], flag_off[RT_MAX_DEVICES];  // byte offsets of slice k and of its exactness flag
+};
+__global__ __launch_bounds__(256) void k_unpack_tiles(const uint8_t* gather, uint8_t* frame, UnpackArgs a) {
+  const int k = (int)blockIdx.y, L = (int)blockIdx.x;
+  if (k >= a.n_rep || L >= a.n_tiles[k]) return;
+  int tx, ty;
+  shard_tile_xy(a.tiles_x, a.S[k], a.si[k], a.sc[k], L, tx, ty);
+  const int x = tx * 16 + (int)(threadIdx.x & 15), y = ty * 16 + (int)(threadIdx.x >> 4);
+  if (x >= a.W || y >= a.H) return;
+  const size_t src = a.off[k] + ((size_t)L * 256 + threadIdx.x) * (size_t)a.E, dst = ((size_t)y * a.W + x) * (size_t)a.E;
+  if (a.E == 3) {
+    frame[dst] = gather[src];
+    frame[dst + 1] = gather[src + 1];
+    frame[dst + 2] = gather[src + 2];
+  } else {  // 4 or 12 bytes, 4-byte aligned (slices start on 16 B)
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(gather + src);
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(frame + dst);
+    for (int w = 0; w < a.E / 4; w++) d4[w] = s4[w];
+  }
+}
+// the 8-bit frame's exactness flags of every replica, OR-ed into the word after the frame
+__global__ void k_or_flags(const uint8_t* gather, UnpackArgs a, uint32_t* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t f = 0;
+  for (int k = 0; k < a.n_rep; k++) f |= *reinterpret_cast<const uint32_t*>(gather + a.flag_off[k]);
+  *out = f;
 }
 
 __global__ void k_debug_math(int op, int n, int in_len, int out_len, const float* in, float* out) {
@@ -580,6 +639,14 @@ void device_release(rt_scene* s) {
     if (b) (void)hipFree(b);
   if (s->asm_buf.h_pack) (void)hipHostFree(s->asm_buf.h_pack);
   s->asm_buf = rt_scene::Assembly{};
+  if (s->dasm.d_gather) (void)hipFree(s->dasm.d_gather);
+  if (s->dasm.d_frame) (void)hipFree(s->dasm.d_frame);
+  if (s->dasm.h_frame) (void)hipHostFree(s->dasm.h_frame);
+  for (void* e : s->dasm.ev_chunk)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
+  s->dasm = rt_scene::DevAssembly{};
+  if (s->asm_ev) (void)hipEventDestroy((hipEvent_t)s->asm_ev);
+  s->asm_ev = nullptr;
   s->d_nodes = nullptr; s->d_nodes4 = nullptr; s->d_tris = nullptr; s->d_fshade = nullptr;
   s->d_refbox = nullptr; s->d_mats = nullptr; s->d_stats = nullptr; s->d_pf_check = nullptr;
   for (int k = 0; k < s->n_slots; k++) {
@@ -591,7 +658,9 @@ void device_release(rt_scene* s) {
     f = rt_scene::FrameSlot{};
   }
   if (s->lpt.d_cost) (void)hipFree(s->lpt.d_cost);
+  if (s->lpt.d_cost2) (void)hipFree(s->lpt.d_cost2);
   if (s->lpt.d_order) (void)hipFree(s->lpt.d_order);
+  if (s->lpt.sort_done) (void)hipEventDestroy((hipEvent_t)s->lpt.sort_done);
   s->lpt = rt_scene::LptMap{};
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
   s->ev_pool.clear();
@@ -1151,20 +1220,31 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   // a race on the order's values only: any order is a permutation)
   const bool lpt = one_wave_kernel && !(variant & 131072) && P.xcd_remap >= 2 && grid > 0 && (alone || (variant & 524288));
   bool lpt_sort = false;
+  int lpt_dilate = 0;
   rt_scene::LptMap& lm = s->lpt;
   if (lpt) {
     const size_t waves = units;
     if (waves > lm.waves) {
       for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
       if (lm.d_cost) (void)hipFree(lm.d_cost);
+      if (lm.d_cost2) (void)hipFree(lm.d_cost2);
       if (lm.d_order) (void)hipFree(lm.d_order);
-      lm.d_cost = lm.d_order = nullptr;
+      lm.d_cost = lm.d_cost2 = lm.d_order = nullptr;
       lm.waves = 0;
       lm.valid = false;
       HIPCHECK(hipMalloc((void**)&lm.d_cost, waves * 4));
+      HIPCHECK(hipMalloc((void**)&lm.d_cost2, waves * 4));
       HIPCHECK(hipMalloc((void**)&lm.d_order, waves * 4));
       lm.waves = waves;
     }
+    if (!lm.sort_done) {
+      hipEvent_t e;
+      HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      lm.sort_done = e;
+    }
+    // the previous lone frame's sort (queued after its frame-done event, on its own stream) may still be running:
+    // this frame reads its order and may overwrite the costs it reads, so its stream waits for it
+    HIPCHECK(hipStreamWaitEvent(st, (hipEvent_t)lm.sort_done, 0));
     const int64_t key[8] = {fr->width, fr->height, si, sc, fr->mode, depth0, P.xcd_remap, (int64_t)waves};
     const bool same = lm.valid && memcmp(key, lm.key, sizeof key) == 0;
     if (same) P.order = lm.d_order;
@@ -1178,6 +1258,10 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     const int refresh = refresh_env ? std::max(1, atoi(refresh_env)) : kLptRefresh;
     const bool key_moved = moved_env ? atoi(moved_env) != 0 : kLptMoved;
     const bool moved = memcmp(cam->view_matrix, lm.view, sizeof lm.view) != 0;
+    // moving: this frame's camera differs from the previous lone frame's -> its costs are dilated before the sort
+    // (whole frames only: the wave grid of a shard is not contiguous). RT_LPT_DILATE: A/B knob (radius, 0 = off)
+    const bool moving = memcmp(cam->view_matrix, lm.prev_view, sizeof lm.prev_view) != 0;
+    memcpy(lm.prev_view, cam->view_matrix, sizeof lm.prev_view);
     lpt_sort = !same || ++lm.age >= refresh || (key_moved && moved);
     lm.frames++;
     if (lpt_sort) {
@@ -1186,6 +1270,10 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       lm.valid = false;  // until this frame's k_order_lpt has been queued
       P.cost = lm.d_cost;
       lm.sorts++;
+      const char* dil_env = debug_env("RT_LPT_DILATE");
+      const int r = dil_env ? std::max(0, std::min(4, atoi(dil_env))) : kLptDilate;
+      lpt_dilate = (moving && sc == 1 && !dual) ? r : 0;
+      if (lpt_dilate) lm.dilated++;
     }
   }
   if (s->ev_used + 3 > s->ev_pool.size()) {  // (init_slots creates kEventFrames frames' worth up front)
@@ -1299,15 +1387,26 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   } else {
     HIPCHECK(hipEventRecord(ev_m, st));
   }
-  if (lpt_sort) {  // the scene's next lone frame of this shape dispatches longest-first
-    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)lm.d_cost, lm.d_order,
-                       (int)units, P.xcd_remap, (variant & 262144) ? 1 : 0);
+  // the frame is done at ev_b; the sort for the scene's next lone frame of this shape follows it on the same
+  // stream, so rt_synchronize (which waits for ev_b) returns without it and the sort overlaps the caller's turn
+  // between two frames (the next lone frame waits for sort_done)
+  HIPCHECK(hipEventRecord(ev_b, st));
+  slot.last_done = ev_b;
+  if (lpt_sort) {
+    const uint32_t* c = lm.d_cost;
+    if (lpt_dilate) {
+      hipLaunchKernelGGL(k_cost_dilate, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, st, (const uint32_t*)lm.d_cost,
+                         lm.d_cost2, P.tiles_x, P.tiles_y, (int)units, lpt_dilate);
+      HIPCHECK(hipGetLastError());
+      c = lm.d_cost2;
+    }
+    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, c, lm.d_order, (int)units, P.xcd_remap,
+                       (variant & 262144) ? 1 : 0);
     HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventRecord((hipEvent_t)lm.sort_done, st));
     lm.valid = true;
     lm.age = 0;
   }
-  HIPCHECK(hipEventRecord(ev_b, st));
-  slot.last_done = ev_b;
   s->last_slot = slot_id;
   s->next_slot = (slot_id + 1) % s->n_slots;
   s->last_W = fr->width;
@@ -1352,7 +1451,11 @@ static int check_prefetch_word(rt_scene* s) {
 static int sync_one(rt_scene* s, rt_stats* out) {
   int rc = check_device_scene(s);
   if (rc) return rc;
-  for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
+  // every frame since the last synchronize has finished: each slot's latest frame-done event (a slot's frames
+  // run in order on its stream); the longest-first sort queued behind a lone frame may still run (its own event)
+  for (int k = 0; k < s->n_slots; k++) {
+    if (s->slots[k].last_done) HIPCHECK(hipEventSynchronize((hipEvent_t)s->slots[k].last_done));
+  }
   if ((rc = check_prefetch_word(s))) return rc;
   struct Reset {
     rt_scene* s;
@@ -1593,6 +1696,174 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
 // devices queued first; then one host worker per device waits for its copy and places the tiles into the
 // caller's frame (rows of 16 pixels). Only the tiles of the replicas' shards are written.
 enum AsmKind { ASM_RGB = 0, ASM_FACE = 1, ASM_T = 2, ASM_RGB8 = 3 };
+
+// Device-side assembly (SURVEY e1 "peer-writes to GPU0"): when the replicas rendered the
+// whole frame between them, each packs its tiles on its own stream and copies them into device 0's gather
+// buffer (hipMemcpyPeerAsync over xGMI; a device copy when replicas share a GPU), device 0 waits for every
+// slice (one event per replica), places all tiles with one kernel (k_unpack_tiles) and copies the frame to
+// pinned host memory in kChunks pieces, which host threads move into the caller's buffer as each lands. The
+// host path below (every device's tiles to the host, rows placed by the host) serves a caller's own shard of
+// the frame.
+static int assemble_device(rt_scene* s, AsmKind kind, void* out, int32_t* exact, const char* what) {
+  const int D = n_replicas(s);
+  const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
+  const size_t E = kind == ASM_RGB ? 12 : kind == ASM_RGB8 ? 3 : 4;
+  UnpackArgs ua;
+  memset(&ua, 0, sizeof ua);
+  ua.n_rep = D, ua.W = W, ua.H = H, ua.tiles_x = tiles_x, ua.E = (int32_t)E;
+  size_t total = 0;
+  int max_tiles = 0;
+  for (int k = 0; k < D; k++) {
+    rt_scene* r = replica(s, k);
+    ua.si[k] = r->last_shard_index;
+    ua.sc[k] = r->last_shard_count;
+    ua.S[k] = frame_super_tile(ua.sc[k]);
+    ua.n_tiles[k] = shard_tile_slots(tiles_x, tiles_y, ua.S[k], ua.si[k], ua.sc[k]);
+    max_tiles = std::max(max_tiles, ua.n_tiles[k]);
+    const size_t bytes = (size_t)ua.n_tiles[k] * 256 * E, flag_at = (bytes + 15) & ~(size_t)15;
+    ua.off[k] = total;
+    ua.flag_off[k] = total + flag_at;
+    total += flag_at + 16;
+  }
+  const size_t frame_bytes = (size_t)W * H * E;
+  rt_scene::DevAssembly& g = s->dasm;
+  HIPCHECK(hipSetDevice(s->device));
+  if (total > g.gather_bytes || frame_bytes + 16 > g.frame_bytes || frame_bytes + 16 > g.h_bytes) {
+    for (int k = 0; k < D; k++) {  // no replica's copy into the old buffers may be in flight
+      rt_scene* r = replica(s, k);
+      HIPCHECK(hipSetDevice(r->device));
+      for (int q = 0; q < r->n_slots; q++) HIPCHECK(hipStreamSynchronize((hipStream_t)r->slots[q].stream));
+    }
+    HIPCHECK(hipSetDevice(s->device));
+    if (total > g.gather_bytes) {
+      if (g.d_gather) (void)hipFree(g.d_gather);
+      g.d_gather = nullptr, g.gather_bytes = 0;
+      HIPCHECK(hipMalloc(&g.d_gather, total));
+      g.gather_bytes = total;
+    }
+    if (frame_bytes + 16 > g.frame_bytes) {
+      if (g.d_frame) (void)hipFree(g.d_frame);
+      g.d_frame = nullptr, g.frame_bytes = 0;
+      HIPCHECK(hipMalloc(&g.d_frame, frame_bytes + 16));
+      g.frame_bytes = frame_bytes + 16;
+    }
+    if (frame_bytes + 16 > g.h_bytes) {
+      if (g.h_frame) (void)hipHostFree(g.h_frame);
+      g.h_frame = nullptr, g.h_bytes = 0;
+      HIPCHECK(hipHostMalloc(&g.h_frame, frame_bytes + 16, hipHostMallocDefault));
+      g.h_bytes = frame_bytes + 16;
+    }
+  }
+  for (int c = 0; c < rt_scene::DevAssembly::kChunks; c++)
+    if (!g.ev_chunk[c]) {
+      hipEvent_t e;
+      HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      g.ev_chunk[c] = e;
+    }
+  uint8_t* gather = (uint8_t*)g.d_gather;
+  // every replica: pack behind its share of the frame; replicas 1.. copy their slice to device 0
+  for (int k = 0; k < D; k++) {
+    rt_scene* r = replica(s, k);
+    HIPCHECK(hipSetDevice(r->device));
+    rt_scene::FrameSlot& f = r->slots[r->last_slot];
+    hipStream_t st = (hipStream_t)f.stream;
+    const size_t need = ua.flag_off[k] - ua.off[k] + 16;
+    uint8_t* dst;
+    if (k == 0) {
+      dst = gather + ua.off[0];
+    } else {
+      rt_scene::Assembly& a = r->asm_buf;
+      if (need > a.bytes) {
+        HIPCHECK(hipStreamSynchronize(st));
+        if (a.d_pack) (void)hipFree(a.d_pack);
+        if (a.h_pack) (void)hipHostFree(a.h_pack);
+        a = rt_scene::Assembly{};
+        HIPCHECK(hipMalloc(&a.d_pack, need));
+        HIPCHECK(hipHostMalloc(&a.h_pack, need, hipHostMallocDefault));
+        a.bytes = need;
+      }
+      dst = (uint8_t*)a.d_pack;
+      if (!r->asm_ev) {
+        hipEvent_t e;
+        HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        r->asm_ev = e;
+      }
+    }
+    if (ua.n_tiles[k] > 0) {
+      if (kind == ASM_RGB8) {
+        uint32_t* flag = (uint32_t*)(dst + (ua.flag_off[k] - ua.off[k]));
+        HIPCHECK(hipMemsetAsync(flag, 0, 4, st));
+        hipLaunchKernelGGL(k_pack_shard, dim3(ua.n_tiles[k]), dim3(256), 0, st, (const float*)f.d_rgb, dst, W, H, tiles_x,
+                           ua.si[k], ua.sc[k], ua.n_tiles[k], ua.S[k], flag);
+      } else {
+        const uint32_t* src = kind == ASM_RGB ? (const uint32_t*)f.d_rgb
+                              : kind == ASM_FACE ? (const uint32_t*)f.d_face : (const uint32_t*)f.d_t;
+        hipLaunchKernelGGL(k_pack_tiles32, dim3(ua.n_tiles[k]), dim3(256), 0, st, src, (uint32_t*)dst, W, H, tiles_x,
+                           ua.si[k], ua.sc[k], ua.n_tiles[k], ua.S[k], kind == ASM_RGB ? 3 : 1);
+      }
+      HIPCHECK(hipGetLastError());
+    } else if (kind == ASM_RGB8) {
+      HIPCHECK(hipMemsetAsync(dst + (ua.flag_off[k] - ua.off[k]), 0, 4, st));
+    }
+    if (k > 0) {
+      if (r->device == s->device) HIPCHECK(hipMemcpyAsync(gather + ua.off[k], dst, need, hipMemcpyDeviceToDevice, st));
+      else HIPCHECK(hipMemcpyPeerAsync(gather + ua.off[k], s->device, dst, r->device, need, st));
+      HIPCHECK(hipEventRecord((hipEvent_t)r->asm_ev, st));
+    }
+  }
+  // device 0: every slice in, tiles placed, the frame to the host in chunks
+  HIPCHECK(hipSetDevice(s->device));
+  hipStream_t st0 = (hipStream_t)s->slots[s->last_slot].stream;
+  for (int k = 1; k < D; k++) HIPCHECK(hipStreamWaitEvent(st0, (hipEvent_t)replica(s, k)->asm_ev, 0));
+  uint8_t* frame = (uint8_t*)g.d_frame;
+  if (max_tiles > 0) {
+    hipLaunchKernelGGL(k_unpack_tiles, dim3((unsigned)max_tiles, (unsigned)D), dim3(256), 0, st0, (const uint8_t*)gather, frame, ua);
+    HIPCHECK(hipGetLastError());
+  }
+  if (kind == ASM_RGB8) {
+    hipLaunchKernelGGL(k_or_flags, dim3(1), dim3(64), 0, st0, (const uint8_t*)gather, ua, (uint32_t*)(frame + frame_bytes));
+    HIPCHECK(hipGetLastError());
+  }
+  const int C = (int)std::max<size_t>(1, std::min<size_t>(rt_scene::DevAssembly::kChunks, frame_bytes >> 21));
+  const size_t cb = ((frame_bytes + C - 1) / C + 63) & ~(size_t)63;
+  auto span = [&](int c, size_t& o, size_t& n) {
+    o = std::min(frame_bytes, (size_t)c * cb);
+    n = std::min(frame_bytes, o + cb) - o;
+  };
+  for (int c = 0; c < C; c++) {
+    size_t o, n;
+    span(c, o, n);
+    const size_t extra = (c == C - 1 && kind == ASM_RGB8) ? 4 : 0;  // the OR-ed flag follows the frame
+    if (n + extra) HIPCHECK(hipMemcpyAsync((uint8_t*)g.h_frame + o, frame + o, n + extra, hipMemcpyDeviceToHost, st0));
+    HIPCHECK(hipEventRecord((hipEvent_t)g.ev_chunk[c], st0));
+  }
+  std::vector<int> ok((size_t)C, 1);
+  auto take = [&](int c) {
+    if (hipEventSynchronize((hipEvent_t)g.ev_chunk[c]) != hipSuccess) { ok[c] = 0; return; }
+    size_t o, n;
+    span(c, o, n);
+    if (n) memcpy((uint8_t*)out + o, (const uint8_t*)g.h_frame + o, n);
+  };
+  std::vector<std::thread> th;
+  for (int c = 1; c < C; c++) {
+    try {
+      th.emplace_back(take, c);
+    } catch (const std::exception&) {
+      take(c);
+    }
+  }
+  take(0);
+  for (auto& t : th) t.join();
+  for (int c = 0; c < C; c++)
+    if (!ok[c]) { set_error("%s: frame copy to the host failed", what); return RT_ERR_HIP; }
+  if (exact) {
+    uint32_t fl = 0;
+    memcpy(&fl, (const uint8_t*)g.h_frame + frame_bytes, 4);
+    *exact = fl ? 0 : 1;
+  }
+  return RT_OK;
+}
+
 static int assemble(rt_scene* s, AsmKind kind, int64_t capacity_pixels, void* out, int32_t* exact, const char* what) {
   const int D = n_replicas(s);
   const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
@@ -1602,6 +1873,31 @@ static int assemble(rt_scene* s, AsmKind kind, int64_t capacity_pixels, void* ou
     set_error("%s: buffers hold %lld pixels, the last frame has %lld (%d x %d)", what, (long long)capacity_pixels,
               (long long)W * H, W, H);
     return RT_ERR_INVALID;
+  }
+  {  // the replicas' frames must be of the scene's last size (and carry hit records for face / t)
+    for (int k = 0; k < D; k++) {
+      rt_scene* r = replica(s, k);
+      int rc = check_device_scene(r);
+      if (rc) return rc;
+      const rt_scene::FrameSlot& f = r->slots[r->last_slot];
+      if (!f.d_rgb || r->last_W != W || r->last_H != H || (size_t)W * H > f.fb_pixels) {
+        set_error("%s: device %d has no frame of the scene's last size", what, r->device);
+        return RT_ERR_INVALID;
+      }
+      if ((kind == ASM_FACE || kind == ASM_T) && !(r->last_flags & RT_FRAME_WRITE_HITS)) {
+        set_error("last frame was rendered without RT_FRAME_WRITE_HITS");
+        return RT_ERR_INVALID;
+      }
+    }
+    // the whole frame split over the replicas (the caller asked for shard 0 of 1): device-side assembly, unless the
+    // A/B knob RT_ASM_HOST asks for the host path
+    const bool whole = s->last_shard_count == D && s->last_shard_index == 0;
+    const char* host_env = debug_env("RT_ASM_HOST");
+    if (whole && !(host_env && atoi(host_env))) {
+      const int rc = assemble_device(s, kind, out, exact, what);
+      HIPCHECK(hipSetDevice(s->device));
+      return rc;
+    }
   }
   struct Job {
     rt_scene* r;

@@ -156,6 +156,20 @@ struct rt_scene {
     void* h_pack = nullptr;  // pinned host copy of it
     size_t bytes = 0;        // capacity of both
   } asm_buf;
+  // Device-side assembly of a multi-device scene's frame (rt_device.hip assemble_device; this scene = device 0):
+  // every replica's packed tiles land in d_gather (peer copies over xGMI), one kernel places them into d_frame,
+  // and one pinned copy brings the frame to the host
+  struct DevAssembly {
+    void* d_gather = nullptr;  // device 0: the replicas' packed slices, one after the other
+    size_t gather_bytes = 0;
+    void* d_frame = nullptr;   // device 0: the assembled frame (+16 B: the 8-bit frame's exactness flag)
+    size_t frame_bytes = 0;
+    void* h_frame = nullptr;   // pinned host copy of d_frame
+    size_t h_bytes = 0;
+    static constexpr int kChunks = 8;
+    void* ev_chunk[kChunks] = {};  // device 0: the device-to-host copy of each chunk has landed
+  } dasm;
+  void* asm_ev = nullptr;  // this replica's packed slice has reached device 0 (an event of this replica's device)
   std::vector<rt_stats> last_device_stats;  // per replica, from the last rt_synchronize of a multi-device scene
   // device buffer sizes (peer replication copies these)
   size_t nodes_bytes = 0, nodes4_bytes = 0, fshade_bytes = 0, refbox_bytes = 0, mats_bytes = 0;
@@ -216,7 +230,10 @@ struct rt_scene {
     bool valid = false;     // d_order holds an order for frames of key
     int age = 0;            // lone frames dispatched with that order since it was computed
     float view[16] = {0};   // the camera of the frame whose costs made the order
-    int64_t sorts = 0, frames = 0;  // lone frames that re-sorted / dispatched longest-first (rt_debug_lpt_stats)
+    float prev_view[16] = {0};  // the camera of the scene's previous lone frame (motion test)
+    uint32_t* d_cost2 = nullptr;  // a moving camera's costs, dilated over neighbouring waves before the sort
+    void* sort_done = nullptr;    // event after the latest sort: the next lone frame waits for it on its stream
+    int64_t sorts = 0, frames = 0, dilated = 0;  // lone frames dispatched longest-first / that re-sorted / dilated
   } lpt;
   static constexpr int kMaxSlots = 4;
   FrameSlot slots[kMaxSlots];

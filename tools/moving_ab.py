@@ -6,7 +6,10 @@ flyscene.cpp:116-127), on a 1-slot and a 4-slot scene, for the longest-first dis
 cost maps were per frame slot). One JSON line per measurement.
 
 Usage: RTAMD_DEBUG_KNOBS=1 python tools/moving_ab.py <soup|bunny> <primary|full> <policy> [frames] [reps]
-  policy: lib (the library as built), moved0 / moved1 (RT_LPT_MOVED), r1 (RT_LPT_REFRESH=1), nolpt (variant 131072)
+  policy: lib (the library as built), moved0 / moved1 (RT_LPT_MOVED), r1 (RT_LPT_REFRESH=1), nolpt (variant 131072),
+          dil0 / dil1 / dil2 (RT_LPT_DILATE: a moving camera's cost map dilated over r waves), exact (every pose
+          rendered twice and the second render timed: its map was recorded at the same pose -- the best an order
+          from wave costs can do on the moving poses)
 """
 import json
 import os
@@ -20,7 +23,9 @@ import bench  # noqa: E402
 scene, mode, policy = sys.argv[1], sys.argv[2], sys.argv[3]
 frames = int(sys.argv[4]) if len(sys.argv) > 4 else 60
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 2
-env = {"moved0": {"RT_LPT_MOVED": "0"}, "moved1": {"RT_LPT_MOVED": "1"}, "r1": {"RT_LPT_REFRESH": "1"}}.get(policy, {})
+env = {"moved0": {"RT_LPT_MOVED": "0"}, "moved1": {"RT_LPT_MOVED": "1"}, "r1": {"RT_LPT_REFRESH": "1"},
+       "dil0": {"RT_LPT_DILATE": "0"}, "dil1": {"RT_LPT_DILATE": "1"}, "dil2": {"RT_LPT_DILATE": "2"},
+       "exact": {"RT_LPT_DILATE": "0"}}.get(policy, {})
 os.environ.update(env)
 rt = bench.load_rtamd()
 import torch  # noqa: E402
@@ -47,15 +52,18 @@ for fif in (1, 4):
                 sc.render_async(path.next() if path else static, rt.DEFAULT_LIGHTS, W, H, mode=m)
                 sc.synchronize()
             cams = path.take(frames) if path else [static] * frames
-            k_ms = tr_ms = 0.0
+            k_ms = tr_ms = el = 0.0
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
             for c in cams:
+                if policy == "exact":  # record this pose's own costs first (untimed)
+                    sc.render_async(c, rt.DEFAULT_LIGHTS, W, H, mode=m)
+                    sc.synchronize()
+                t0 = time.perf_counter()
                 sc.render_async(c, rt.DEFAULT_LIGHTS, W, H, mode=m)
                 st = sc.synchronize()
+                el += time.perf_counter() - t0
                 k_ms += st["kernel_ms"]
                 tr_ms += st["trace_kernel_ms"]
-            el = time.perf_counter() - t0
             rec = {"lib": lib, "policy": policy, "scene": scene, "mode": mode, "fif": fif, "rep": rep, "camera": cam_kind,
                    "frames": frames, "mrays_per_s_one_at_a_time": round(W * H * frames / el / 1e6, 1),
                    "frame_ms_wall": round(el / frames * 1e3, 4), "kernel_ms": round(tr_ms / frames, 4),
