@@ -437,7 +437,8 @@ int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float* cert_origi
  * variant renders the same bits. Returns the previous value. */
 int rt_debug_set_variant(int32_t v);
 /* Diagnostics: on = 1 lets the library read its A/B and diagnostic environment knobs (RT_KERNEL_VARIANT,
- * RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_TIMELINE_SPLIT, RT_XCD_RUN, RT_LDS_PAD, RT_LPT_REFRESH, RT_LPT_MOVED, RT_SAH_TRAV, RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING); by default
+ * RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_TIMELINE_SPLIT, RT_XCD_RUN, RT_LDS_PAD, RT_LPT_REFRESH, RT_LPT_MOVED,
+ * RT_LPT_DILATE, RT_ASM_DEVICE, RT_SAH_TRAV, RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING); by default
  * (and after on = 0) it ignores the process environment, so a drop-in's trees, kernels and dispatch never
  * depend on it. Turning it on also takes RT_KERNEL_VARIANT as the current kernel variant. */
 int rt_debug_env_knobs(int32_t on);
@@ -452,7 +453,8 @@ int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64
 /* Raw counters of the last RT_FRAME_STATS frame (diagnostics), out[0..n): 0 node visits, 1 triangle tests,
  * 2 wave node fetches, 3 wave triangle fetches, 4 primary rays, 5 hits, 6 total rays, 7 wave stack pops,
  * 8 pops at which no lane that wanted the entry still could reach it before its closest hit (closest-hit
- * traversal only); entries past the last counter are 0. */
+ * traversal only); 48..63: the FULL kernel's packet walks by phase (csrc/rt_kernels.h ST_PW .. ST_PH); entries past
+ * the last counter are 0. */
 int rt_debug_counters(rt_scene* s, int64_t n, int64_t* out);
 
 /* Longest-first dispatch of lone frames (diagnostics): out3[0] = lone frames dispatched with the scene's cost

@@ -29,7 +29,7 @@ namespace rt {
 // bits.
 constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
 constexpr bool kLptMoved = true;  // re-sort after every lone frame whose camera moved since the map's frame
-constexpr int kLptDilate = 1;     // a moving camera's map: each wave's cost = the max over (2r+1)^2 waves around it
+constexpr int kLptDilate = 2;     // a moving camera's map: each wave's cost = the max over (2r+1)^2 waves around it
 constexpr int kSplitK = 1536;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k); round 5
                                // re-sweep without the spill: 1536 +2.5..6% over 2048 (profiles/ab/r05_c5_split_ab.txt)
 constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
@@ -1697,13 +1697,12 @@ extern "C" int rt_synchronize(rt_scene* s, rt_stats* out) {
 // caller's frame (rows of 16 pixels). Only the tiles of the replicas' shards are written.
 enum AsmKind { ASM_RGB = 0, ASM_FACE = 1, ASM_T = 2, ASM_RGB8 = 3 };
 
-// Device-side assembly (SURVEY e1 "peer-writes to GPU0"): when the replicas rendered the
-// whole frame between them, each packs its tiles on its own stream and copies them into device 0's gather
-// buffer (hipMemcpyPeerAsync over xGMI; a device copy when replicas share a GPU), device 0 waits for every
-// slice (one event per replica), places all tiles with one kernel (k_unpack_tiles) and copies the frame to
-// pinned host memory in kChunks pieces, which host threads move into the caller's buffer as each lands. The
-// host path below (every device's tiles to the host, rows placed by the host) serves a caller's own shard of
-// the frame.
+// Device-side assembly (SURVEY e1 "peer-writes to GPU0"; A/B knob RT_ASM_DEVICE, see assemble):
+// when the replicas rendered the whole frame between them, each packs its tiles on its own stream and copies
+// them into device 0's gather buffer (hipMemcpyPeerAsync over xGMI; a device copy when replicas share a GPU),
+// device 0 waits for every slice (one event per replica), places all tiles with one kernel (k_unpack_tiles)
+// and copies the frame to pinned host memory in kChunks pieces, which host threads move into the caller's
+// buffer as each lands.
 static int assemble_device(rt_scene* s, AsmKind kind, void* out, int32_t* exact, const char* what) {
   const int D = n_replicas(s);
   const int W = s->last_W, H = s->last_H, tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
@@ -1889,11 +1888,14 @@ static int assemble(rt_scene* s, AsmKind kind, int64_t capacity_pixels, void* ou
         return RT_ERR_INVALID;
       }
     }
-    // the whole frame split over the replicas (the caller asked for shard 0 of 1): device-side assembly, unless the
-    // A/B knob RT_ASM_HOST asks for the host path
+    // The host path below is the default: with the replicas on distinct GPUs every device copies its own tiles
+    // over its own PCIe link at once, where the device-side assembly funnels the whole frame through device 0's
+    // link. With replicas sharing one GPU (the only measurable case here: one link either way) the two measured
+    // level -- 8 replicas, 4K 8-bit frame: 1.10-1.36 vs 1.21-1.27 ms (profiles/ab/r06_assembly_ab.txt). The
+    // device-side path (the whole frame split over the replicas) is kept behind the A/B knob RT_ASM_DEVICE.
     const bool whole = s->last_shard_count == D && s->last_shard_index == 0;
-    const char* host_env = debug_env("RT_ASM_HOST");
-    if (whole && !(host_env && atoi(host_env))) {
+    const char* dev_env = debug_env("RT_ASM_DEVICE");
+    if (whole && dev_env && atoi(dev_env)) {
       const int rc = assemble_device(s, kind, out, exact, what);
       HIPCHECK(hipSetDevice(s->device));
       return rc;

@@ -150,8 +150,14 @@ enum { ST_NODE = 0, ST_TRI, ST_WNODE, ST_WTRI, ST_RAYS, ST_HITS, ST_TOTAL, ST_WP
        // wave's lanes of the steps / tests whose node the lane entered, summed over regions) -- what a wave
        // walking those regions one ray per lane would spend
        ST_HN0, ST_HL0 = ST_HN0 + 7, ST_HPN = ST_HL0 + 7, ST_HPT = ST_HPN + 3, ST_HLN = ST_HPT + 3, ST_HLT = ST_HLN + 3,
-       ST_COUNT = ST_HLT + 3 };
-constexpr int kStatSlots = 64;
+       // round 6: the FULL megakernel's packet walks by phase p (0 primary, 1 shadows of the
+       // primary hits, 2 reflection, 3 shadows of the reflection hits): walks with some active lane (ST_PW + p), the
+       // active lanes at their entry summed (ST_PL + p), their node steps (ST_PS + p) and triangle tests (ST_PT + p);
+       // ST_PH + b: the secondary phases' node steps by the walk's active lanes at entry (1-8, 9-16, 17-32, 33-48,
+       // 49-64)
+       ST_PW = ST_HLT + 3, ST_PL = ST_PW + 4, ST_PS = ST_PL + 4, ST_PT = ST_PS + 4, ST_PH = ST_PT + 4,
+       ST_COUNT = ST_PH + 5 };
+constexpr int kStatSlots = 80;
 static_assert(ST_COUNT <= kStatSlots, "stat slots");
 constexpr int kHybridK[3] = {4, 8, 16};
 __device__ __forceinline__ int lane_bin(uint32_t n) { return n == 0 ? 0 : n == 1 ? 1 : n < 4 ? 2 : n < 8 ? 3 : n < 16 ? 4 : n < 32 ? 5 : 6; }
@@ -1407,13 +1413,37 @@ void k_primary_fused(FrameParams P) {
 // SPLIT: mixed-octant secondary packets walk once per octant (trace_oct); the small-scene build only --
 // measured C5 +1.5% at 4 frames in flight, +1..3% one at a time, the 1M soup in FULL -5%
 // (profiles/ab/r03_full_split_oct_ab.txt)
+// counting run: one phase's packet walk(s) of a wave (ST_PW ..)
+struct PhaseMark {
+  uint32_t n0, t0;
+};
+template <bool STATS>
+__device__ __forceinline__ PhaseMark phase_begin(const uint32_t* cnt) {
+  if (!STATS) return PhaseMark{0, 0};
+  return PhaseMark{cnt[ST_WNODE], cnt[ST_WTRI]};
+}
+template <bool STATS>
+__device__ __forceinline__ void phase_end(uint32_t* cnt, int p, const PhaseMark& m, bool act) {
+  if (!STATS) return;
+  const uint64_t b = ballot(act);
+  if (b == 0) return;
+  const uint32_t lanes = (uint32_t)__popcll(b), steps = cnt[ST_WNODE] - m.n0;
+  cnt[ST_PW + p]++;
+  cnt[ST_PL + p] += lanes;
+  cnt[ST_PS + p] += steps;
+  cnt[ST_PT + p] += cnt[ST_WTRI] - m.t0;
+  if (p > 0) cnt[ST_PH + (lanes <= 8 ? 0 : lanes <= 16 ? 1 : lanes <= 32 ? 2 : lanes <= 48 ? 3 : 4)] += steps;
+}
+
 template <bool STATS, int TRAV, bool SPLIT = false>
 __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, bool active, WaveLds<TRAV, STATS>& lds, int wv,
                                          uint32_t* cnt, Hit& h, uint32_t& face0) {
   h = Hit{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
   // the primary packet is coherent: octant-specialised loops
+  PhaseMark pm = phase_begin<STATS>(cnt);
   trace_oct<false, STATS, TRAV>(P.sc, r, active, h, dummy, lds, wv, cnt);
+  phase_end<STATS>(cnt, 0, pm, active);
   const bool hit0 = active && h.t != INFINITY;
   if (STATS && hit0) cnt[ST_HITS]++;
 
@@ -1431,7 +1461,9 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   }
   // the primary hits' shadow packets head for the same light from neighbouring points: octant loops for
   // them too (A/B knob RT_FULL_OCT_SHADOW); the reflection hits' shadows keep the generic loop
+  pm = phase_begin<STATS>(cnt);
   const f3 direct0 = calc_color<true, STATS, TRAV, true, SPLIT>(P, st, hi0, r.o, hit0, &lds, wv, cnt);
+  phase_end<STATS>(cnt, 1, pm, hit0);
   if (hit0 && hi0.mat != -1) st.ks = load_mat(P.sc.mats[hi0.mat]).ks;  // traceRay :355-358
 
   // reflect(dir.normalized(), interpolateNormal(...)), offset 0.001 (flyscene.cpp:361-363)
@@ -1443,7 +1475,9 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   setup_cull(rr, P.sc.static_pad);
   if (STATS && hit0) cnt[ST_TOTAL]++;
   Hit h1{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  pm = phase_begin<STATS>(cnt);
   trace_oct<false, STATS, TRAV, false, SPLIT>(P.sc, rr, hit0, h1, dummy, lds, wv, cnt);
+  phase_end<STATS>(cnt, 2, pm, hit0);
   const bool hit1 = hit0 && h1.t != INFINITY;
   HitInfo hi1;
   hi1.mat = -1;
@@ -1455,7 +1489,9 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
     hi1.p = f3{rr.o.x + h1.t * rr.d.x, rr.o.y + h1.t * rr.d.y, rr.o.z + h1.t * rr.d.z};
     hi1.n = hit_normal(P.sc, tr1, h1.slot, hi1.p, hi1.mat);
   }
+  pm = phase_begin<STATS>(cnt);
   const f3 direct1 = calc_color<true, STATS, TRAV, true, SPLIT>(P, st, hi1, rr.o, hit1, &lds, wv, cnt);
+  phase_end<STATS>(cnt, 3, pm, hit1);
   if (hit1) {
     if (hi1.mat != -1) st.ks = load_mat(P.sc.mats[hi1.mat]).ks;
     // depth 1: direct1 + traceRay(depth 2)=0 * ks, clamped

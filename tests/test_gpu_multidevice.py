@@ -157,9 +157,8 @@ def test_caller_shard_on_multi_device_scene(rt, soup):
 
 
 def test_rgb8_download_matches_one_device(rt, bunny):
-    """f3 output path on a multi-device scene: the 8-bit frame assembled on device 0 from the devices' packed
-    tiles (device-side assembly, the default for a whole frame) equals the one-device frame's, with the exactness
-    flag."""
+    """f3 output path on a multi-device scene: the 8-bit frame assembled from the devices' packed tiles equals the
+    one-device frame's, with the exactness flag."""
     W, H = 1920, 1080
     cam = rt.flycam(W, H, 0, 0, 20)
     out = []
@@ -171,22 +170,22 @@ def test_rgb8_download_matches_one_device(rt, bunny):
 
 
 @pytest.fixture
-def host_assembly(rt):
-    """The multi-device frame assembled on the host (RT_ASM_HOST, a debug knob) instead of on device 0."""
+def device_assembly(rt):
+    """The multi-device frame assembled on device 0 (RT_ASM_DEVICE, an A/B knob) instead of on the host."""
     rt.lib().rt_debug_env_knobs(1)
-    os.environ["RT_ASM_HOST"] = "1"
+    os.environ["RT_ASM_DEVICE"] = "1"
     try:
         yield
     finally:
-        os.environ.pop("RT_ASM_HOST", None)
+        os.environ.pop("RT_ASM_DEVICE", None)
         rt.lib().rt_debug_env_knobs(1 if os.environ.get("RTAMD_DEBUG_KNOBS") == "1" else 0)
 
 
 @pytest.mark.parametrize("case", ["C4", "C5"])
-def test_host_and_device_assembly_agree(rt, soup, bunny, host_assembly, case):
-    """Both assembly paths of a multi-device scene: device-side (the default for a whole frame:
-    peer copies to device 0, one unpack kernel, one copy to the host) and host-side (every device's tiles to the
-    host) give the one-device frame bit for bit -- float rgb, face, t and the 8-bit frame with its flag."""
+def test_device_side_assembly_matches_one_device(rt, soup, bunny, device_assembly, case):
+    """The device-side assembly of a multi-device scene (peer copies of every replica's packed
+    tiles to device 0, one unpack kernel, one chunked copy to the host) gives the one-device frame bit for bit --
+    float rgb, face, t and the 8-bit frame with its flag -- like the host-side assembly the other tests run."""
     d = DIG[case]
     W, H = d["W"], d["H"]
     mode = "primary" if case == "C4" else "full"
@@ -196,7 +195,7 @@ def test_host_and_device_assembly_agree(rt, soup, bunny, host_assembly, case):
     m = rt.RT_MODE_FULL if mode == "full" else rt.RT_MODE_PRIMARY
     src["one"].render(rt.flycam(W, H, 0, 0, 20), rt.DEFAULT_LIGHTS, W, H, mode=m)
     ref8 = src["one"].download_rgb8(W, H)
-    got = frame(rt, multi, W, H, mode)  # host path (the fixture's knob)
+    got = frame(rt, multi, W, H, mode)  # device-side path (the fixture's knob)
     got8 = multi.download_rgb8(W, H)
     for a, b in zip(one[:3], got[:3]):
         assert np.asarray(a).tobytes() == np.asarray(b).tobytes()

@@ -47,17 +47,17 @@ for s in $STEPS; do
       unset RTAMD_DEBUG_KNOBS
       python3 tools/moving_summary.py $OUT/moving.jsonl ;;
     asm)
-      # multi-device frame assembly, device-side (default) against host-side (RT_ASM_HOST), 2 and 8 replicas of the
-      # scene on the box's one GPU; interleaved reps
+      # multi-device frame assembly, host-side (default) against device-side (RT_ASM_DEVICE), 2 and 8 replicas of
+      # the scene on the box's one GPU; interleaved reps
       export RTAMD_DEBUG_KNOBS=1
       for rep in 1 2; do
         for d in 0,0 0,0,0,0,0,0,0,0; do
           n=$(echo $d | tr ',' ' ' | wc -w)
           for h in 0 1; do
-            RT_ASM_HOST=$h timeout -k 10 300 python bench.py --gpus $n --devices $d --steps 20 --warmup 5 --no-cpu --no-extra \
+            RT_ASM_DEVICE=$h timeout -k 10 300 python bench.py --gpus $n --devices $d --steps 20 --warmup 5 --no-cpu --no-extra \
                 > $OUT/asm_${n}_h${h}_r$rep.json 2> $OUT/asm_${n}_h${h}_r$rep.err
             rc=$?; [ $rc -ne 0 ] && { echo "asm $n h$h rc=$rc"; hard $rc; exit $rc; }
-            python3 -c "import json;d=json.loads(open('$OUT/asm_${n}_h${h}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('asm n$n host$h r$rep', d['value'], d['ms_per_step'], c.get('e2e_frame_ms'), c.get('assembly_ms'), d.get('parity',{}).get('face_t_digest_equal'))"
+            python3 -c "import json;d=json.loads(open('$OUT/asm_${n}_h${h}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('asm n$n device$h r$rep', d['value'], d['ms_per_step'], c.get('e2e_frame_ms'), c.get('assembly_ms'), d.get('parity',{}).get('face_t_digest_equal'))"
           done
         done
       done
