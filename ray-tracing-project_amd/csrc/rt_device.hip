@@ -40,7 +40,27 @@ __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c, int shift) {
   const int b = (q < 0 ? 0 : (q > 4 * 8 - 1 ? 4 * 8 - 1 : q)) >> shift;
   return (uint32_t)((kLptBuckets >> shift) - 1 - b);
 }
-__global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost, uint32_t* order, int n, int C, int shift) {
+// A moving camera's cost map (the reference's Flycamera moves every frame a key is held): between two frames the
+// image shifts by about a wave (C5's bunny: ~9 pixels per 0.01-unit step), so the waves an earlier frame found
+// costly sit next to the ones that will be. With dilate = r > 0 (whole frames: logical wave j = 4 * tile +
+// quarter, tile t = ty * tiles_x + tx) each wave's cost is taken as the maximum recorded cost over the
+// (2r + 1) x (2r + 1) waves around it in the frame's grid of 8x8-pixel waves, so the longest-first order and the
+// split of the costliest waves cover where the costly region moves to. Counts live in LDS, one column per
+// thread (a register array indexed by the bucket compiled to a waterfall loop per access).
+__device__ __forceinline__ uint32_t lpt_cost(const uint32_t* cost, int j, int n, int tiles_x, int tiles_y, int r) {
+  if (r <= 0 || j >= 4 * tiles_x * tiles_y) return cost[j];
+  const int t = j >> 2, q = j & 3;
+  const int wx = (t % tiles_x) * 2 + (q & 1), wy = (t / tiles_x) * 2 + (q >> 1), gw = 2 * tiles_x, gh = 2 * tiles_y;
+  uint32_t m = 0;
+  for (int y = max(0, wy - r); y <= min(gh - 1, wy + r); y++)
+    for (int x = max(0, wx - r); x <= min(gw - 1, wx + r); x++) {
+      const int k = 4 * ((y >> 1) * tiles_x + (x >> 1)) + (y & 1) * 2 + (x & 1);
+      if (k < n) m = max(m, cost[k]);
+    }
+  return m;
+}
+__global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost, uint32_t* order, int n, int C, int shift,
+                                                           int tiles_x, int tiles_y, int dilate) {
   __shared__ uint32_t cnt[kLptBuckets][kLptThreads];
   __shared__ uint32_t base[kLptBuckets];
   const int x = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -54,10 +74,8 @@ __global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost,
     const int k = p >> 3;
     return (k / C) * 8 * C + x * C + (k % C);
   };
-  uint32_t mine[kLptBuckets];
-  for (int b = 0; b < kLptBuckets; b++) mine[b] = 0;
-  for (int r = r0; r < r1; r++) mine[lpt_bucket(cost[item(r)], shift)]++;
-  for (int b = 0; b < nb; b++) cnt[b][t] = mine[b];
+  for (int b = 0; b < nb; b++) cnt[b][t] = 0;
+  for (int r = r0; r < r1; r++) cnt[lpt_bucket(lpt_cost(cost, item(r), n, tiles_x, tiles_y, dilate), shift)][t]++;
   __syncthreads();
   // exclusive scan of each bucket's per-thread counts: wave w scans buckets w, w + 8, ..; lane i owns
   // threads 8i .. 8i + 7
@@ -79,37 +97,12 @@ __global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost,
     for (int b = 0; b < nb; b++) { const uint32_t v = base[b]; base[b] = s; s += v; }
   }
   __syncthreads();
-  for (int b = 0; b < nb; b++) mine[b] = base[b] + cnt[b][t];
   for (int r = r0; r < r1; r++) {
     const int j = item(r);
-    const uint32_t rr = mine[lpt_bucket(cost[j], shift)]++;
+    const uint32_t b = lpt_bucket(lpt_cost(cost, j, n, tiles_x, tiles_y, dilate), shift);
+    const uint32_t rr = base[b] + cnt[b][t]++;
     order[8 * rr + x] = (uint32_t)j;
   }
-}
-
-// A moving camera's cost map (the reference's Flycamera moves every frame a key is held): between two frames the
-// image shifts by about a wave (C5's bunny: ~9 pixels per 0.01-unit step), so the waves an earlier frame found
-// costly sit next to the ones that will be. Before the sort, each wave takes the maximum recorded cost over the
-// (2r+1) x (2r+1) waves around it in the frame's wave grid (8x8-pixel waves; whole frames only: logical wave
-// j = 4 * tile + quarter, tile t = ty * tiles_x + tx), so the longest-first order and the split of the costliest
-// waves cover where the costly region moves to.
-__global__ __launch_bounds__(256) void k_cost_dilate(const uint32_t* cost, uint32_t* out, int tiles_x, int tiles_y, int n, int r) {
-  const int j = (int)(blockIdx.x * 256u + threadIdx.x);
-  if (j >= n) return;
-  const int t = j >> 2, q = j & 3;
-  const int wx = (t % tiles_x) * 2 + (q & 1), wy = (t / tiles_x) * 2 + (q >> 1), gw = 2 * tiles_x, gh = 2 * tiles_y;
-  uint32_t m = 0;
-  for (int dy = -r; dy <= r; dy++) {
-    const int y = wy + dy;
-    if (y < 0 || y >= gh) continue;
-    for (int dx = -r; dx <= r; dx++) {
-      const int x = wx + dx;
-      if (x < 0 || x >= gw) continue;
-      const int k = 4 * ((y >> 1) * tiles_x + (x >> 1)) + (y & 1) * 2 + (x & 1);
-      if (k < n) m = max(m, cost[k]);
-    }
-  }
-  out[j] = m;
 }
 
 // RT_MODE_BOX_COLORS, once per colour set: for every face id, color += box->color over the reference
@@ -658,7 +651,6 @@ void device_release(rt_scene* s) {
     f = rt_scene::FrameSlot{};
   }
   if (s->lpt.d_cost) (void)hipFree(s->lpt.d_cost);
-  if (s->lpt.d_cost2) (void)hipFree(s->lpt.d_cost2);
   if (s->lpt.d_order) (void)hipFree(s->lpt.d_order);
   if (s->lpt.sort_done) (void)hipEventDestroy((hipEvent_t)s->lpt.sort_done);
   s->lpt = rt_scene::LptMap{};
@@ -1227,13 +1219,11 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     if (waves > lm.waves) {
       for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
       if (lm.d_cost) (void)hipFree(lm.d_cost);
-      if (lm.d_cost2) (void)hipFree(lm.d_cost2);
       if (lm.d_order) (void)hipFree(lm.d_order);
-      lm.d_cost = lm.d_cost2 = lm.d_order = nullptr;
+      lm.d_cost = lm.d_order = nullptr;
       lm.waves = 0;
       lm.valid = false;
       HIPCHECK(hipMalloc((void**)&lm.d_cost, waves * 4));
-      HIPCHECK(hipMalloc((void**)&lm.d_cost2, waves * 4));
       HIPCHECK(hipMalloc((void**)&lm.d_order, waves * 4));
       lm.waves = waves;
     }
@@ -1393,15 +1383,8 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   HIPCHECK(hipEventRecord(ev_b, st));
   slot.last_done = ev_b;
   if (lpt_sort) {
-    const uint32_t* c = lm.d_cost;
-    if (lpt_dilate) {
-      hipLaunchKernelGGL(k_cost_dilate, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, st, (const uint32_t*)lm.d_cost,
-                         lm.d_cost2, P.tiles_x, P.tiles_y, (int)units, lpt_dilate);
-      HIPCHECK(hipGetLastError());
-      c = lm.d_cost2;
-    }
-    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, c, lm.d_order, (int)units, P.xcd_remap,
-                       (variant & 262144) ? 1 : 0);
+    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)lm.d_cost, lm.d_order, (int)units,
+                       P.xcd_remap, (variant & 262144) ? 1 : 0, P.tiles_x, P.tiles_y, lpt_dilate);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord((hipEvent_t)lm.sort_done, st));
     lm.valid = true;
