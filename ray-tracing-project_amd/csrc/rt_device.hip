@@ -40,27 +40,13 @@ __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c, int shift) {
   const int b = (q < 0 ? 0 : (q > 4 * 8 - 1 ? 4 * 8 - 1 : q)) >> shift;
   return (uint32_t)((kLptBuckets >> shift) - 1 - b);
 }
-// A moving camera's cost map (the reference's Flycamera moves every frame a key is held): between two frames the
-// image shifts by about a wave (C5's bunny: ~9 pixels per 0.01-unit step), so the waves an earlier frame found
-// costly sit next to the ones that will be. With dilate = r > 0 (whole frames: logical wave j = 4 * tile +
-// quarter, tile t = ty * tiles_x + tx) each wave's cost is taken as the maximum recorded cost over the
-// (2r + 1) x (2r + 1) waves around it in the frame's grid of 8x8-pixel waves, so the longest-first order and the
-// split of the costliest waves cover where the costly region moves to. Counts live in LDS, one column per
-// thread (a register array indexed by the bucket compiled to a waterfall loop per access).
-__device__ __forceinline__ uint32_t lpt_cost(const uint32_t* cost, int j, int n, int tiles_x, int tiles_y, int r) {
-  if (r <= 0 || j >= 4 * tiles_x * tiles_y) return cost[j];
-  const int t = j >> 2, q = j & 3;
-  const int wx = (t % tiles_x) * 2 + (q & 1), wy = (t / tiles_x) * 2 + (q >> 1), gw = 2 * tiles_x, gh = 2 * tiles_y;
-  uint32_t m = 0;
-  for (int y = max(0, wy - r); y <= min(gh - 1, wy + r); y++)
-    for (int x = max(0, wx - r); x <= min(gw - 1, wx + r); x++) {
-      const int k = 4 * ((y >> 1) * tiles_x + (x >> 1)) + (y & 1) * 2 + (x & 1);
-      if (k < n) m = max(m, cost[k]);
-    }
-  return m;
-}
-__global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost, uint32_t* order, int n, int C, int shift,
-                                                           int tiles_x, int tiles_y, int dilate) {
+// The sort reads `cost` (the recording frame's per-wave costs, or with a moving camera their dilation: the
+// render kernel's waves raised cost_dil over their neighbourhoods, wave_clock_end) and clears what it read in
+// both arrays, so the next recording frame starts from zeros -- the atomic maxima of split sub-waves and of the
+// dilation need them -- without a fill on the frame's own critical path. Counts live in LDS, one column per
+// thread (a register array indexed by the bucket compiled to a waterfall loop per access: 15 us per sort).
+__global__ __launch_bounds__(kLptThreads) void k_order_lpt(uint32_t* cost, uint32_t* clear2, uint32_t* order, int n, int C,
+                                                           int shift) {
   __shared__ uint32_t cnt[kLptBuckets][kLptThreads];
   __shared__ uint32_t base[kLptBuckets];
   const int x = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -75,7 +61,7 @@ __global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost,
     return (k / C) * 8 * C + x * C + (k % C);
   };
   for (int b = 0; b < nb; b++) cnt[b][t] = 0;
-  for (int r = r0; r < r1; r++) cnt[lpt_bucket(lpt_cost(cost, item(r), n, tiles_x, tiles_y, dilate), shift)][t]++;
+  for (int r = r0; r < r1; r++) cnt[lpt_bucket(cost[item(r)], shift)][t]++;
   __syncthreads();
   // exclusive scan of each bucket's per-thread counts: wave w scans buckets w, w + 8, ..; lane i owns
   // threads 8i .. 8i + 7
@@ -92,16 +78,23 @@ __global__ __launch_bounds__(kLptThreads) void k_order_lpt(const uint32_t* cost,
     if (lane == 63) base[b] = incl;  // bucket total
   }
   __syncthreads();
-  if (t == 0) {  // bucket totals -> start ranks, longest bucket first
-    uint32_t s = 0;
-    for (int b = 0; b < nb; b++) { const uint32_t v = base[b]; base[b] = s; s += v; }
+  if (wv == 0) {  // bucket totals -> start ranks, longest bucket first (one lane per bucket)
+    const uint32_t v = lane < nb ? base[lane] : 0u;
+    uint32_t incl = v;
+    for (int off = 1; off < 32; off <<= 1) {
+      const uint32_t o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    if (lane < nb) base[lane] = incl - v;
   }
   __syncthreads();
   for (int r = r0; r < r1; r++) {
     const int j = item(r);
-    const uint32_t b = lpt_bucket(lpt_cost(cost, j, n, tiles_x, tiles_y, dilate), shift);
+    const uint32_t b = lpt_bucket(cost[j], shift);
     const uint32_t rr = base[b] + cnt[b][t]++;
     order[8 * rr + x] = (uint32_t)j;
+    cost[j] = 0u;
+    if (clear2) clear2[j] = 0u;
   }
 }
 
@@ -651,6 +644,7 @@ void device_release(rt_scene* s) {
     f = rt_scene::FrameSlot{};
   }
   if (s->lpt.d_cost) (void)hipFree(s->lpt.d_cost);
+  if (s->lpt.d_cost_dil) (void)hipFree(s->lpt.d_cost_dil);
   if (s->lpt.d_order) (void)hipFree(s->lpt.d_order);
   if (s->lpt.sort_done) (void)hipEventDestroy((hipEvent_t)s->lpt.sort_done);
   s->lpt = rt_scene::LptMap{};
@@ -1219,12 +1213,16 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     if (waves > lm.waves) {
       for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
       if (lm.d_cost) (void)hipFree(lm.d_cost);
+      if (lm.d_cost_dil) (void)hipFree(lm.d_cost_dil);
       if (lm.d_order) (void)hipFree(lm.d_order);
-      lm.d_cost = lm.d_order = nullptr;
+      lm.d_cost = lm.d_cost_dil = lm.d_order = nullptr;
       lm.waves = 0;
       lm.valid = false;
       HIPCHECK(hipMalloc((void**)&lm.d_cost, waves * 4));
+      HIPCHECK(hipMalloc((void**)&lm.d_cost_dil, waves * 4));
       HIPCHECK(hipMalloc((void**)&lm.d_order, waves * 4));
+      HIPCHECK(hipMemsetAsync(lm.d_cost, 0, waves * 4, st));  // (each sort clears what it read after this)
+      HIPCHECK(hipMemsetAsync(lm.d_cost_dil, 0, waves * 4, st));
       lm.waves = waves;
     }
     if (!lm.sort_done) {
@@ -1252,7 +1250,15 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     // (whole frames only: the wave grid of a shard is not contiguous). RT_LPT_DILATE: A/B knob (radius, 0 = off)
     const bool moving = memcmp(cam->view_matrix, lm.prev_view, sizeof lm.prev_view) != 0;
     memcpy(lm.prev_view, cam->view_matrix, sizeof lm.prev_view);
-    lpt_sort = !same || ++lm.age >= refresh || (key_moved && moved);
+    // Measured under the reference's moving camera (profiles/ab/r06_moving_camera_ab.txt, one frame at a time):
+    // an L2-resident scene whose lone frames split their costliest waves (C5: the bunny's silhouette tiles) loses
+    // the split's gain with a map even one frame old (0.38 ms against 0.227 with an exact map) and regains most
+    // of it with a fresh, dilated map (0.31 ms); the soup's per-wave costs decorrelate within a frame of motion
+    // (fresh or 8 frames old, dilated or not: 0.233-0.237 ms, no map 0.245), so large scenes keep the 8-frame
+    // refresh and spend no sort per frame. (RT_LPT_MOVED forces either rule.)
+    const bool l2_small = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
+    const bool resort_on_motion = moved_env ? key_moved : (key_moved && l2_small);
+    lpt_sort = !same || ++lm.age >= refresh || (resort_on_motion && moved);
     lm.frames++;
     if (lpt_sort) {
       memcpy(lm.key, key, sizeof key);
@@ -1262,8 +1268,12 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       lm.sorts++;
       const char* dil_env = debug_env("RT_LPT_DILATE");
       const int r = dil_env ? std::max(0, std::min(4, atoi(dil_env))) : kLptDilate;
-      lpt_dilate = (moving && sc == 1 && !dual) ? r : 0;
-      if (lpt_dilate) lm.dilated++;
+      lpt_dilate = (moving && resort_on_motion && sc == 1 && !dual) ? r : 0;
+      if (lpt_dilate) {
+        lm.dilated++;
+        P.cost_dil = lm.d_cost_dil;
+        P.dil_r = lpt_dilate;
+      }
     }
   }
   if (s->ev_used + 3 > s->ev_pool.size()) {  // (init_slots creates kEventFrames frames' worth up front)
@@ -1306,8 +1316,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       const bool small_p = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes || debug_env("RT_SPLIT_KP_ANY");
       P.split_k = (P.order && small_p && (!P.timeline || timeline_split) && kTraceWPB == 1)
                       ? std::max(0, std::min<int>(split_p, (int)(units / 4))) & ~7 : 0;
-      if (P.cost && P.split_k)
-        HIPCHECK(hipMemsetAsync(P.cost, 0, units * 4, st));  // sub-waves add / take the max
+      // (sub-waves take the max into the cost map, which the previous sort left at zero)
       const dim3 g(grid * (4 / kTraceWPB) + 3 * P.split_k), b(64 * kTraceWPB);
       // RT_LDS_PAD (diagnostics): extra dynamic LDS per block, to cap the resident waves per CU in
       // occupancy experiments (160 KiB / (pad + 1 KiB) blocks per CU)
@@ -1362,8 +1371,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
         P.split_k = std::max(0, std::min<int>(split_env, (int)(units / 4))) & ~7;
       else
         P.split_k = 0;
-      if (P.cost && P.split_k)
-        HIPCHECK(hipMemsetAsync(P.cost, 0, units * 4, st));  // sub-waves add / take the max
+      // (sub-waves take the max into the cost map, which the previous sort left at zero)
       if (stats) { if (hits) launch_full<true, true>(P, grid, st, trav, small); else launch_full<true, false>(P, grid, st, trav, small); }
       else { if (hits) launch_full<false, true>(P, grid, st, trav, small); else launch_full<false, false>(P, grid, st, trav, small); }
       HIPCHECK(hipEventRecord(ev_m, st));
@@ -1383,8 +1391,9 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   HIPCHECK(hipEventRecord(ev_b, st));
   slot.last_done = ev_b;
   if (lpt_sort) {
-    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, (const uint32_t*)lm.d_cost, lm.d_order, (int)units,
-                       P.xcd_remap, (variant & 262144) ? 1 : 0, P.tiles_x, P.tiles_y, lpt_dilate);
+    uint32_t* in = lpt_dilate ? lm.d_cost_dil : lm.d_cost;
+    hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, in, lpt_dilate ? lm.d_cost : (uint32_t*)nullptr,
+                       lm.d_order, (int)units, P.xcd_remap, (variant & 262144) ? 1 : 0);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord((hipEvent_t)lm.sort_done, st));
     lm.valid = true;

@@ -239,6 +239,11 @@ struct FrameParams {
   // chunked-XCD order. cost[logical wave] receives the wave's duration in shader cycles (null = off).
   const uint32_t* order;
   uint32_t* cost;
+  // a moving camera's cost map (whole frames, rt_device.hip render_one): each wave also raises cost_dil over the
+  // (2 dil_r + 1)^2 waves around it in the frame's wave grid (atomic max), so the next frame's order sees each
+  // wave's neighbourhood maximum; null = off
+  uint32_t* cost_dil;
+  int32_t dil_r;
   // k_render_full with an order: the first split_k logical waves of the order (the costliest of an
   // earlier frame) run as four 16-lane sub-waves each (blocks 0 .. 4 split_k - 1), the rest whole; the
   // grid is then (logical waves + 3 split_k) blocks. 0 = off.

@@ -1279,11 +1279,24 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
   // split waves far above the rest and coarsens the order's buckets, -20% on C5 lone frames; keeping the
   // stale cost is within 1% of the maximum but never refreshes it; running cost-recording frames unsplit
   // costs 6%)
-  if (P.cost && lane == 0) {
+  if (P.cost) {
     const uint64_t dt = t1 - w.t0;
     const uint32_t c = dt > 0x3FFFFFFFull ? 0x3FFFFFFFu : (uint32_t)dt;
-    if (!sub_wave) P.cost[qw] = c;
-    else atomicMax(P.cost + qw, c);
+    if (lane == 0) {
+      if (!sub_wave) P.cost[qw] = c;
+      else atomicMax(P.cost + qw, c);
+    }
+    // a moving camera: lane i < (2r + 1)^2 raises the map at the wave's i-th neighbour (whole frames: tile qw / 4
+    // sits at (tile % tiles_x, tile / tiles_x), its quarters 2 x 2 waves)
+    if (P.cost_dil) {
+      const int r = P.dil_r, d = 2 * r + 1;
+      if (lane < d * d) {
+        const int t = qw >> 2, q = qw & 3;
+        const int x = (t % P.tiles_x) * 2 + (q & 1) + lane % d - r, y = (t / P.tiles_x) * 2 + (q >> 1) + lane / d - r;
+        if (x >= 0 && y >= 0 && x < 2 * P.tiles_x && y < 2 * P.tiles_y)
+          atomicMax(P.cost_dil + 4 * ((y >> 1) * P.tiles_x + (x >> 1)) + (y & 1) * 2 + (x & 1), c);
+      }
+    }
   }
   if (!P.timeline) return;
   const uint32_t r1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
