@@ -279,6 +279,8 @@ typedef struct rt_frame {
 #define RT_FRAME_STATS 2      /* counting run: per-ray node visits / triangle tests (slower) */
 #define RT_FRAME_TIMELINE 4   /* diagnostics: each wave of the render kernel records its start / end clocks
                                  and the CU it ran on (rt_debug_timeline); PRIMARY and FULL kernels */
+#define RT_FRAME_WAVE_STATS 8 /* diagnostics, with RT_FRAME_STATS: each wave of the counting run also records its own
+                                 counts (rt_debug_wave_stats) */
 
 typedef struct rt_stats {
   double kernel_ms;         /* device time of the render kernels since the previous rt_synchronize,
@@ -456,6 +458,13 @@ int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64
  * traversal only); 48..63: the FULL kernel's packet walks by phase (csrc/rt_kernels.h ST_PW .. ST_PH); entries past
  * the last counter are 0. */
 int rt_debug_counters(rt_scene* s, int64_t n, int64_t* out);
+
+/* Per-wave counts of the last frame rendered with RT_FRAME_STATS | RT_FRAME_WAVE_STATS (diagnostics), indexed by
+ * logical wave (tile * 4 + quarter), 8 words each: PRIMARY node steps, triangle tests, hit lanes, 0 x 5; FULL the
+ * node steps of its four packet phases (primary, shadows of the primary hits, reflection, shadows of the
+ * reflection hits), then their triangle tests. *n_waves = the frame's logical waves; capacity_waves smaller than
+ * that -> RT_ERR_INVALID. */
+int rt_debug_wave_stats(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64_t* n_waves);
 
 /* Longest-first dispatch of lone frames (diagnostics): out3[0] = lone frames dispatched with the scene's cost
  * map since the scene was created, out3[1] = of them, frames that re-sorted the map from their own wave costs

@@ -637,7 +637,7 @@ void device_release(rt_scene* s) {
   s->d_refbox = nullptr; s->d_mats = nullptr; s->d_stats = nullptr; s->d_pf_check = nullptr;
   for (int k = 0; k < s->n_slots; k++) {
     rt_scene::FrameSlot& f = s->slots[k];
-    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline};
+    void* fb[] = {f.d_rgb, f.d_face, f.d_t, f.d_hits, f.d_rgb8, f.d_full, f.d_queue, f.d_timeline, f.d_wave_stats};
     for (void* b : fb)
       if (b) (void)hipFree(b);
     release_slot_stream(s->device, f.stream, f.dedicated_queue);
@@ -982,6 +982,22 @@ extern "C" int rt_debug_timeline(rt_scene* s, int64_t capacity_waves, uint32_t* 
   return RT_OK;
 }
 
+extern "C" int rt_debug_wave_stats(rt_scene* s, int64_t capacity_waves, uint32_t* out8, int64_t* n_waves) {
+  int rc = check_device_scene(s);
+  if (rc) return rc;
+  const rt_scene::FrameSlot& f = s->slots[s->last_slot];
+  if (!(s->last_flags & RT_FRAME_WAVE_STATS) || !(s->last_flags & RT_FRAME_STATS) || !f.d_wave_stats) {
+    set_error("rt_debug_wave_stats: last frame had no RT_FRAME_STATS | RT_FRAME_WAVE_STATS");
+    return RT_ERR_INVALID;
+  }
+  if (n_waves) *n_waves = s->last_wave_stats_waves;
+  if (!out8) return RT_OK;
+  if (capacity_waves < s->last_wave_stats_waves) { set_error("rt_debug_wave_stats: buffer too small"); return RT_ERR_INVALID; }
+  HIPCHECK(hipStreamSynchronize((hipStream_t)f.stream));
+  HIPCHECK(hipMemcpy(out8, f.d_wave_stats, (size_t)s->last_wave_stats_waves * 32, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
 extern "C" int rt_debug_counters(rt_scene* s, int64_t n, int64_t* out) {
   int rc = check_device_scene(s);
   if (rc) return rc;
@@ -1144,6 +1160,20 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     HIPCHECK(hipMemsetAsync(slot.d_timeline, 0, waves * 32, st));
     P.timeline = slot.d_timeline;
     s->last_timeline_waves = (int64_t)waves;
+  }
+  if (stats && (fr->flags & RT_FRAME_WAVE_STATS)) {  // per logical wave (tile * 4 + quarter)
+    const size_t lw = (size_t)grid * 4;
+    if (lw > slot.wave_stats_waves) {
+      HIPCHECK(hipStreamSynchronize(st));
+      if (slot.d_wave_stats) (void)hipFree(slot.d_wave_stats);
+      slot.d_wave_stats = nullptr;
+      slot.wave_stats_waves = 0;
+      HIPCHECK(hipMalloc((void**)&slot.d_wave_stats, lw * 32));
+      slot.wave_stats_waves = lw;
+    }
+    HIPCHECK(hipMemsetAsync(slot.d_wave_stats, 0, lw * 32, st));
+    P.wave_stats = slot.d_wave_stats;
+    s->last_wave_stats_waves = (int64_t)lw;
   }
   if (fr->mode == RT_MODE_FULL && (variant & 16)) {
     if (sc > 1) { set_error("rt_render: the FULL stage-pipeline variant renders whole frames only"); return RT_ERR_UNSUPPORTED; }

@@ -244,6 +244,8 @@ struct FrameParams {
   // wave's neighbourhood maximum; null = off
   uint32_t* cost_dil;
   int32_t dil_r;
+  // RT_FRAME_WAVE_STATS (a counting frame, diagnostics): 8 words per logical wave (rt_debug_wave_stats)
+  uint32_t* wave_stats;
   // k_render_full with an order: the first split_k logical waves of the order (the costliest of an
   // earlier frame) run as four 16-lane sub-waves each (blocks 0 .. 4 split_k - 1), the rest whole; the
   // grid is then (logical waves + 3 split_k) blocks. 0 = off.

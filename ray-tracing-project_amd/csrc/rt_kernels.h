@@ -1308,6 +1308,19 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
   }
 }
 
+// RT_FRAME_WAVE_STATS: this wave's own counts (PRIMARY: node steps, triangle tests, hit lanes; FULL: node steps of
+// the four phases, then their triangle tests), for the per-wave time breakdown (tools/wave_breakdown.py)
+__device__ __forceinline__ void wave_stats_out(const FrameParams& P, const uint32_t* cnt, int lane, int qw, bool full) {
+  if (!P.wave_stats || lane != 0) return;
+  uint32_t* o = P.wave_stats + 8 * (size_t)qw;
+  if (full) {
+    for (int p = 0; p < 4; p++) { o[p] = cnt[ST_PS + p]; o[4 + p] = cnt[ST_PT + p]; }
+  } else {
+    o[0] = cnt[ST_WNODE]; o[1] = cnt[ST_WTRI]; o[2] = cnt[ST_HITS]; o[3] = 0;
+    o[4] = o[5] = o[6] = o[7] = 0;
+  }
+}
+
 __device__ __forceinline__ void flush_stats(const FrameParams& P, const uint32_t* cnt, int lane) {
 #pragma unroll
   for (int c = 0; c < ST_COUNT; c++) {
@@ -1341,7 +1354,15 @@ void k_trace_primary(FrameParams P) {
     const uint32_t nh = (uint32_t)__popcll(ballot(c.active && h.t != INFINITY));
     if (c.lane == 0) P.wcount0[c.qw] = nh;
   }
-  if (STATS) flush_stats(P, cnt, c.lane);
+  if (STATS) {
+    if (P.wave_stats) {  // the wave's hit lanes (ST_HITS counts per lane)
+      uint32_t w[ST_COUNT];
+      for (int k = 0; k < ST_COUNT; k++) w[k] = cnt[k];
+      w[ST_HITS] = (uint32_t)__popcll(ballot(c.active && h.t != INFINITY));
+      wave_stats_out(P, w, c.lane, c.qw, false);
+    }
+    flush_stats(P, cnt, c.lane);
+  }
 }
 
 // PRIMARY stage 2: traceRay at depth limit 1 without shadows: calculateColor (flyscene.cpp:603-614)
@@ -1574,7 +1595,10 @@ void k_render_full(FrameParams P) {
       P.t_out[pix] = h.t;
     }
   }
-  if (STATS) flush_stats(P, cnt, (int)lane);
+  if (STATS) {
+    wave_stats_out(P, cnt, (int)lane, c.qw, true);
+    flush_stats(P, cnt, (int)lane);
+  }
   wave_clock_end(P, lds.clk, (int)lane, c.qw, c.sub >= 0);
 }
 

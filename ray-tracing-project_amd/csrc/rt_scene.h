@@ -216,6 +216,8 @@ struct rt_scene {
     uint32_t* d_queue = nullptr;  // persistent-threads variant: 8 per-XCD work counters
     uint32_t* d_timeline = nullptr;  // RT_FRAME_TIMELINE records (8 words per wave)
     size_t timeline_waves = 0;
+    uint32_t* d_wave_stats = nullptr;  // RT_FRAME_WAVE_STATS records (8 words per logical wave)
+    size_t wave_stats_waves = 0;
   };
   // Longest-first dispatch of lone frames (rt_device.hip render_one): the per-wave costs of a recording frame
   // and the order k_order_lpt computed from them, valid for frames with the same key. One map per scene, not
@@ -243,6 +245,7 @@ struct rt_scene {
   int64_t last_rays = 0, last_total_rays = 0;
   int64_t rays_key[4] = {-1, -1, -1, -1}, rays_of_key = 0;  // primary rays of a frame shape (W, H, shard)
   int64_t last_timeline_waves = 0;  // waves recorded by the last RT_FRAME_TIMELINE frame
+  int64_t last_wave_stats_waves = 0;  // logical waves of the last RT_FRAME_WAVE_STATS frame
   bool pending = false;
 };
 

@@ -18,6 +18,7 @@ RT_MODE_BOX_COLORS = 2  # RENDER_BOUNDINGBOX_COLORED_TRIANGLES (flyscene.hpp:166
 RT_FRAME_WRITE_HITS = 1
 RT_FRAME_STATS = 2
 RT_FRAME_TIMELINE = 4
+RT_FRAME_WAVE_STATS = 8
 RT_DEVICE_NONE = -2
 
 # Every symbol include/rt/rt_api.h declares (checked by tests/test_abi.py)
@@ -33,7 +34,7 @@ EXPORTS = [
     "rt_trace_closest_normal", "rt_trace_color", "rt_debug_ray", "rt_version_string", "rt_source_hash",
     "rt_debug_timeline", "rt_debug_counters", "rt_box_colors_random", "rt_scene_set_box_colors", "rt_frame_shard_tiles",
     "rt_debug_record_layout", "rt_debug_scene_flags", "rt_debug_env_knobs", "rt_debug_tree_cost",
-    "rt_synchronize_devices", "rt_debug_lpt_stats",
+    "rt_synchronize_devices", "rt_debug_lpt_stats", "rt_debug_wave_stats",
 ]
 RT_MAX_DEVICES = 16
 RT_DEVICES_ALL = -1
@@ -154,8 +155,9 @@ def lib():
             L.rt_debug_env_knobs(1)
         L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_debug_counters.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
-        if hasattr(L, "rt_debug_lpt_stats"):  # (API 4 libraries of round 5, loaded for A/B, lack it)
+        if hasattr(L, "rt_debug_lpt_stats"):  # (API 4 libraries of round 5, loaded for A/B, lack these)
             L.rt_debug_lpt_stats.argtypes = [vp, C.POINTER(C.c_int64)]
+            L.rt_debug_wave_stats.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
         L.rt_frame_download_rgb8.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int32)]
         L.rt_write_ppm_rgb8.argtypes = [C.c_char_p, vp, C.c_int32, C.c_int32]
@@ -376,6 +378,14 @@ class Scene:
         out = (C.c_int64 * 3)()
         check(lib().rt_debug_lpt_stats(self.h, out))
         return {"frames": int(out[0]), "sorts": int(out[1]), "valid": bool(out[2])}
+
+    def wave_stats(self):
+        """Per-wave counts of the last RT_FRAME_STATS | RT_FRAME_WAVE_STATS frame: uint32 [logical waves, 8]."""
+        n = C.c_int64(0)
+        check(lib().rt_debug_wave_stats(self.h, 0, None, C.byref(n)))
+        out = np.zeros((n.value, 8), np.uint32)
+        check(lib().rt_debug_wave_stats(self.h, n.value, _p(out), C.byref(n)))
+        return out
 
     def counters(self, n=16):
         """Raw counters of the last RT_FRAME_STATS frame (rt_debug_counters): int64 [n]."""

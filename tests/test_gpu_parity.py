@@ -626,6 +626,31 @@ def test_longest_first_dispatch_order(rt):
             assert (cls[o] == pos % 8).all()                 # every wave keeps its XCD position class
 
 
+def test_wave_stats_sum_to_frame_counters(rt):
+    """RT_FRAME_WAVE_STATS (the per-wave breakdown's input, tools/wave_breakdown.py): each logical wave's own
+    counts add up to the counting run's frame totals -- PRIMARY node steps / triangle records / hits, FULL the
+    packet phases' node steps and triangle tests (rt_debug_counters ST_PS / ST_PT)."""
+    mesh = rt.Mesh.load_obj(scene_path("bunny.obj"))
+    sc = rt.Scene(mesh, frames_in_flight=1)
+    W, H = 640, 360
+    cam = rt.flycam(W, H, 0, 0, 20)
+    st = sc.render(cam, rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS | rt.RT_FRAME_WAVE_STATS)[1]
+    ws = sc.wave_stats().astype(np.int64)
+    assert len(ws) == 4 * ((W + 15) // 16) * ((H + 15) // 16)
+    assert ws[:, 0].sum() == st["wave_node_fetches"] and ws[:, 1].sum() == st["wave_tri_fetches"]
+    assert ws[:, 2].sum() == st["hits"] and (ws[:, 2] <= 64).all()
+    sc.render(cam, rt.DEFAULT_LIGHTS, W, H, mode=rt.RT_MODE_FULL, flags=rt.RT_FRAME_STATS | rt.RT_FRAME_WAVE_STATS)
+    ws = sc.wave_stats().astype(np.int64)
+    c = sc.counters(80)
+    ST_PS, ST_PT = 48 + 8, 48 + 12
+    assert [int(ws[:, p].sum()) for p in range(4)] == c[ST_PS:ST_PS + 4]
+    assert [int(ws[:, 4 + p].sum()) for p in range(4)] == c[ST_PT:ST_PT + 4]
+    assert c[ST_PS] > 0 and c[ST_PS + 2] > 0  # primary and reflection walks happened
+    with pytest.raises(rt.RTError):  # a frame without the flag has no per-wave record
+        sc.render(cam, rt.DEFAULT_LIGHTS, W, H)
+        sc.wave_stats()
+
+
 def test_split_costliest_waves(rt, soup):
     """Lone FULL frames dispatched longest-first trace their costliest waves (FrameParams::split_k) as four
     16-lane sub-waves each: every frame after a slot's first (which has no wave costs yet) must still
