@@ -10,6 +10,9 @@ mkdir -p $OUT
 # (clock = GRBM_GUI_ACTIVE / 8 / duration); only the bench frame's launches (no second frame size)
 ARGS="${BENCH_ARGS:---steps 20 --warmup 5 --no-cpu --no-extra --no-e2e --no-side --frames-in-flight 1}"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_avail.txt 2>&1 || true
+# the in-kernel clock of the same workload (timeline frames: s_memtime / s_memrealtime), the issue fractions' clock
+timeout -k 10 120 python3 tools/kernel_clock.py $OUT/kernel_clock.json $ARGS > $OUT/kernel_clock.log 2>&1
+rc=$?; echo "kernel clock rc=$rc"; case $rc in 124|134|137|139) exit $rc;; esac
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
     python3 bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace.err
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc

@@ -17,6 +17,74 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md: max engine clock
+
+
+def issue_block(out, mean, avg_ns, clock=None):
+    """Clock and issue roofline of one kernel. The clock the issue fractions use:
+    * the in-kernel clock when measured (clock = tools/kernel_clock.py's record: median over the waves of a
+      timeline frame of the same workload of delta s_memtime / delta s_memrealtime x 100 MHz, the method of
+      MI355X_MICROARCH.md "DVFS give-back" item 6);
+    * else GRBM_GUI_ACTIVE / 8 / the trace's kernel duration, capped at the chip's 2.4 GHz: that quotient counts
+      the counter window, which on dispatches shorter than ~0.3 ms is longer than the kernel, so it reads high
+      (C2's 70-us kernel: 2.88 GHz) -- kept as grbm_quotient_GHz, not used above the cap.
+    Issue capacity per cycle: one wave64 VALU instruction per 2 cycles per SIMD (4 SIMDs per CU), one SALU / one
+    SMEM instruction per cycle per CU (MI355X_MICROARCH.md); the fractions are over clock x kernel duration.
+    SQ_WAVE_CYCLES and the SQ_WAIT / ACTIVE counters are in quad-cycles."""
+    if "GRBM_GUI_ACTIVE" not in mean or not avg_ns:
+        return
+    q = mean["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+    out["grbm_quotient_GHz"] = round(q, 4)
+    if clock and clock.get("clock_GHz"):
+        clk, src = float(clock["clock_GHz"]), "in-kernel: median over waves of d(s_memtime) / d(s_memrealtime) x 100 MHz (" + \
+            str(clock.get("what", "timeline frame")) + ")"
+    elif q > MAX_CLOCK_GHZ:
+        clk, src = MAX_CLOCK_GHZ, f"GRBM_GUI_ACTIVE / 8 / kernel duration = {q:.2f} GHz reads above the 2.4 GHz maximum " \
+            "(counter window longer than a short dispatch): capped at 2.4, so the issue fractions are lower bounds"
+    else:
+        clk, src = q, "GRBM_GUI_ACTIVE / 8 / kernel duration"
+    out["effective_clock_GHz"] = clk
+    out["clock_source"] = src
+    cyc = avg_ns * clk
+    issue = {"clock_GHz": round(clk, 3), "kernel_ns": round(avg_ns, 1)}
+    if "SQ_INSTS_VALU" in mean:
+        issue["valu_per_launch"] = mean["SQ_INSTS_VALU"]
+        issue["valu_frac"] = round(mean["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 4)
+    if "SQ_INSTS_SALU" in mean:
+        issue["salu_per_launch"] = mean["SQ_INSTS_SALU"]
+        issue["salu_frac"] = round(mean["SQ_INSTS_SALU"] / (256 * cyc), 4)
+    if "SQ_INSTS_SMEM" in mean:
+        issue["smem_frac"] = round(mean["SQ_INSTS_SMEM"] / (256 * cyc), 4)
+    if "SQ_WAVE_CYCLES" in mean:
+        issue["mean_resident_waves_per_simd"] = round(4 * mean["SQ_WAVE_CYCLES"] / (1024 * cyc), 2)
+        for k, name in (("SQ_WAIT_ANY", "wave_cycles_waiting"), ("SQ_ACTIVE_INST_ANY", "wave_cycles_issuing"),
+                        ("SQ_WAIT_INST_ANY", "wave_cycles_issue_stalled")):
+            if k in mean:
+                issue[name] = round(mean[k] / mean["SQ_WAVE_CYCLES"], 4)
+    out["issue"] = issue
+    if "valu_frac" in issue and "wave_cycles_waiting" in issue:
+        out["limiter"] = (f"latency: waves wait on memory (s_waitcnt) {100 * issue['wave_cycles_waiting']:.0f}% "
+                          f"of their cycles and issue in {100 * issue.get('wave_cycles_issuing', 0):.0f}%; "
+                          f"VALU issue at {100 * issue['valu_frac']:.0f}% and SALU at "
+                          f"{100 * issue.get('salu_frac', 0):.0f}% of peak; HBM at "
+                          f"{100 * out.get('hbm_bytes_per_launch', 0) / avg_ns / 8000:.1f}% of 8 TB/s")
+
+
+def refresh(paths):
+    """Recompute the clock / issue / limiter fields of committed profiles/*_pmc.json from their stored counters
+    (the clock rule above; files without GRBM_GUI_ACTIVE are left as they are)."""
+    for p in paths:
+        d = json.load(open(p))
+        mean, avg_ns = d.get("counters_mean_per_dispatch") or {}, d.get("avg_kernel_ns_trace")
+        if "GRBM_GUI_ACTIVE" not in mean or not avg_ns:
+            continue
+        for k in ("issue", "limiter", "effective_clock_GHz", "clock_source", "grbm_quotient_GHz"):
+            d.pop(k, None)
+        issue_block(d, mean, avg_ns, d.get("kernel_clock"))
+        json.dump(d, open(p, "w"), indent=1)
+        print(os.path.basename(p), d["effective_clock_GHz"], d.get("grbm_quotient_GHz"))
+
+
 def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     if kernel is None:  # the bench line's dominant kernel, non-counting instantiation
@@ -72,38 +140,16 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
         out["hbm_write_bytes_per_launch"] = write
         if avg_ns:
             out["hbm_GBps"] = (fetch + write) / avg_ns
-    # Clock and issue roofline. GRBM_GUI_ACTIVE counts busy GPU cycles summed over the 8 XCDs; the
-    # profile is taken with one frame on the GPU at a time (tools/profile.sh: --frames-in-flight 1), so
-    # the trace's kernel duration is the duration the counters saw and GRBM/8 / duration = the clock.
-    # Issue capacity per cycle: one wave64 VALU instruction per 2 cycles per SIMD-32 (4 SIMDs per CU),
-    # one SALU / one SMEM instruction per cycle per CU (MI355X_MICROARCH.md); SQ_WAVE_CYCLES and the
-    # SQ_WAIT / ACTIVE counters are in quad-cycles.
-    if "GRBM_GUI_ACTIVE" in mean and avg_ns:
-        clk = mean["GRBM_GUI_ACTIVE"] / 8 / avg_ns
-        out["effective_clock_GHz"] = clk
-        cyc = avg_ns * clk
-        issue = {"clock_GHz": round(clk, 3), "kernel_ns": round(avg_ns, 1)}
-        if "SQ_INSTS_VALU" in mean:
-            issue["valu_per_launch"] = mean["SQ_INSTS_VALU"]
-            issue["valu_frac"] = round(mean["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 4)
-        if "SQ_INSTS_SALU" in mean:
-            issue["salu_per_launch"] = mean["SQ_INSTS_SALU"]
-            issue["salu_frac"] = round(mean["SQ_INSTS_SALU"] / (256 * cyc), 4)
-        if "SQ_INSTS_SMEM" in mean:
-            issue["smem_frac"] = round(mean["SQ_INSTS_SMEM"] / (256 * cyc), 4)
-        if "SQ_WAVE_CYCLES" in mean:
-            issue["mean_resident_waves_per_simd"] = round(4 * mean["SQ_WAVE_CYCLES"] / (1024 * cyc), 2)
-            for k, name in (("SQ_WAIT_ANY", "wave_cycles_waiting"), ("SQ_ACTIVE_INST_ANY", "wave_cycles_issuing"),
-                            ("SQ_WAIT_INST_ANY", "wave_cycles_issue_stalled")):
-                if k in mean:
-                    issue[name] = round(mean[k] / mean["SQ_WAVE_CYCLES"], 4)
-        out["issue"] = issue
-        if "valu_frac" in issue and "wave_cycles_waiting" in issue:
-            out["limiter"] = (f"latency: waves wait on memory (s_waitcnt) {100 * issue['wave_cycles_waiting']:.0f}% "
-                              f"of their cycles and issue in {100 * issue.get('wave_cycles_issuing', 0):.0f}%; "
-                              f"VALU issue at {100 * issue['valu_frac']:.0f}% and SALU at "
-                              f"{100 * issue.get('salu_frac', 0):.0f}% of peak; HBM at "
-                              f"{100 * out.get('hbm_bytes_per_launch', 0) / avg_ns / 8000:.1f}% of 8 TB/s")
+    clock = None
+    cf = os.path.join(prof, "kernel_clock.json")  # tools/kernel_clock.py, written by tools/profile.sh
+    if os.path.exists(cf):
+        try:
+            clock = json.load(open(cf))
+        except ValueError:
+            clock = None
+    if clock:
+        out["kernel_clock"] = clock
+    issue_block(out, mean, avg_ns, clock)
     if "SQ_WAVE_CYCLES" in mean:
         wc = mean["SQ_WAVE_CYCLES"]
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
@@ -128,4 +174,7 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), kernel=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    if sys.argv[1:2] == ["--refresh"]:
+        refresh(sys.argv[2:])
+    else:
+        main(*sys.argv[1:])
