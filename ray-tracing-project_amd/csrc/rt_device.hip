@@ -407,6 +407,9 @@ static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // 
 // device's queues are oversubscribed and the hardware time-slices them -- eight replicas of one scene on one GPU
 // (32 dedicated queues) ran 2.3x slower than two (profiles/ab/r05_queue_probe.txt) -- so further slots take the
 // pool. dedicated_slots counts the live dedicated queues per device (released by release_slot_stream).
+// A deliberate exception to the per-process GPU_MAX_HW_QUEUES pool: it is what lets one process's
+// frames in flight overlap; the cap is per process, so several renderer processes sharing one GPU each add up
+// to 8 -- the 4-ranks-on-one-GPU rehearsal with and without (RT_SLOT_POOL) is in profiles/ab/r06_slot_queues_ab.txt.
 constexpr int kDedicatedSlotQueues = 8;
 static std::mutex g_slot_mu;
 static int g_dedicated_slots[64] = {};
@@ -416,7 +419,9 @@ static hipStream_t slot_stream(int dev, bool* dedicated) {
   hipStream_t st = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_slot_mu);
-    if (dev >= 0 && dev < 64 && g_dedicated_slots[dev] < kDedicatedSlotQueues &&
+    // (RT_SLOT_POOL, A/B knob: every slot on the runtime's pooled queues, as an ordinary stream)
+    const char* pool_env = debug_env("RT_SLOT_POOL");
+    if (!(pool_env && atoi(pool_env)) && dev >= 0 && dev < 64 && g_dedicated_slots[dev] < kDedicatedSlotQueues &&
         hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) {
       std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
       if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) {

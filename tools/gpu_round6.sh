@@ -62,6 +62,33 @@ for s in $STEPS; do
         done
       done
       unset RTAMD_DEBUG_KNOBS ;;
+    slotq)
+      # frame-slot streams on dedicated hardware queues (default) vs the runtime's pool (RT_SLOT_POOL=1): 2 and 4
+      # torchrun ranks sharing the box's GPU (gloo timing reductions), and the single-process C3 / C5 lines
+      export RTAMD_DEBUG_KNOBS=1
+      for rep in 1 2; do
+        for pool in 0 1; do
+          for n in 2 4; do
+            RT_SLOT_POOL=$pool BENCH_DEVICE=0 BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+                --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n + 10 * pool)) bench.py --gpus $n \
+                --steps 20 --warmup 5 --no-cpu --no-e2e > $OUT/slotq_n${n}_p${pool}_r$rep.json 2> $OUT/slotq_n${n}_p${pool}_r$rep.err
+            rc=$?; [ $rc -ne 0 ] && { echo "slotq n$n pool$pool rc=$rc"; tail -5 $OUT/slotq_n${n}_p${pool}_r$rep.err; hard $rc; exit $rc; }
+            python3 -c "import json;d=json.loads(open('$OUT/slotq_n${n}_p${pool}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('slotq n$n pool$pool r$rep', d['value'], d['ms_per_step'], [p['kernel_ms_per_frame'] for p in c['per_gpu']])"
+          done
+          for sc in soup:primary bunny:full; do
+            IFS=: read scn md <<< "$sc"
+            RT_SLOT_POOL=$pool timeout -k 10 120 python bench.py --scene $scn --mode $md --steps 20 --warmup 5 --no-cpu --no-side \
+                --no-extra --no-e2e --no-stats --no-cold --no-moving > $OUT/slotq_1_${scn}_p${pool}_r$rep.json 2> $OUT/slotq_1_${scn}_p${pool}_r$rep.err
+            rc=$?; [ $rc -ne 0 ] && { echo "slotq 1 $scn rc=$rc"; hard $rc; exit $rc; }
+            python3 -c "import json;d=json.loads(open('$OUT/slotq_1_${scn}_p${pool}_r$rep.json').read().strip().splitlines()[-1]);print('slotq 1proc $scn pool$pool r$rep', d['value'], d['ms_per_step'])"
+          done
+        done
+      done
+      unset RTAMD_DEBUG_KNOBS ;;
+    cli)
+      # the drop-in CLI (host/main.cpp) on the C3 scene: scene setup time with the library default builders
+      timeout -k 10 300 python tools/cli_c3.py > $OUT/cli_c3.json 2> $OUT/cli_c3.err
+      rc=$?; echo "cli rc=$rc"; cat $OUT/cli_c3.json; hard $rc ;;
     hybrid)
       # the counting run's packet -> per-lane hybrid model (C3 soup, C2 bunny)
       timeout -k 10 300 python tools/hybrid_model.py soup bunny > $OUT/hybrid_model.jsonl 2> $OUT/hybrid_model.err
