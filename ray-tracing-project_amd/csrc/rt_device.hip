@@ -3,7 +3,14 @@
 // rt_variants.hip); this file instantiates the product kernels, holds the non-template kernels (dispatch
 // order, box colours, output path, known-answer tests) and the host glue (scene upload, frame dispatch,
 // ray-list queries).
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/file.h>
+#include <unistd.h>
+
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -411,6 +418,53 @@ static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // 
 // frames in flight overlap; the cap is per process, so several renderer processes sharing one GPU each add up
 // to 8 -- the 4-ranks-on-one-GPU rehearsal with and without (RT_SLOT_POOL) is in profiles/ab/r06_slot_queues_ab.txt.
 constexpr int kDedicatedSlotQueues = 8;
+// The same cap across the processes that share a GPU (counted per process only, four renderer processes
+// on one GPU held 32 dedicated queues and ran 4.1x slower than with every slot on the pool --
+// profiles/ab/r06_slot_queues_ab.txt). A lock file per physical GPU (/tmp/rtamd_hwq_<PCI bus id>) lists
+// "pid count" of the processes holding dedicated slot queues on it; entries of processes that no longer exist are
+// dropped, and the file is removed when no holder is left. Without the file (no /tmp, another user's file) a
+// process keeps its own cap only.
+constexpr int kDedicatedSlotQueuesPerGpu = 8;
+static bool hwq_registry(int dev, int delta) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, dev) != hipSuccess) { (void)hipGetLastError(); return delta < 0; }
+  std::string path = "/tmp/rtamd_hwq_";
+  for (const char* c = bus; *c; c++) path += (isalnum((unsigned char)*c) ? *c : '_');
+  const int fd = open(path.c_str(), O_RDWR | O_CREAT, 0666);
+  if (fd < 0) return delta < 0;
+  struct Close { int fd; ~Close() { flock(fd, LOCK_UN); close(fd); } } close_{fd};
+  if (flock(fd, LOCK_EX) != 0) return delta < 0;
+  std::string text;
+  char buf[4096];
+  ssize_t n;
+  while ((n = read(fd, buf, sizeof buf)) > 0) text.append(buf, (size_t)n);
+  const long me = (long)getpid();
+  long mine = 0, others = 0;
+  std::string out;
+  size_t pos = 0;
+  while (pos < text.size()) {
+    const size_t e = std::min(text.find('\n', pos), text.size());
+    long pid = 0, cnt = 0;
+    if (sscanf(text.c_str() + pos, "%ld %ld", &pid, &cnt) == 2 && pid > 0 && cnt > 0) {
+      if (pid == me) mine = cnt;
+      else if (kill((pid_t)pid, 0) == 0 || errno == EPERM) { others += cnt; out += std::to_string(pid) + " " + std::to_string(cnt) + "\n"; }
+    }
+    pos = e + 1;
+  }
+  bool ok = true;
+  if (delta > 0 && others + mine + delta > kDedicatedSlotQueuesPerGpu) ok = false;
+  else mine = std::max(0L, mine + delta);
+  if (mine > 0) out += std::to_string(me) + " " + std::to_string(mine) + "\n";
+  if (out.empty()) {  // no holder left: leave nothing behind (a process waiting on the old file re-counts alone)
+    (void)unlink(path.c_str());
+    return ok;
+  }
+  if (ftruncate(fd, 0) == 0 && lseek(fd, 0, SEEK_SET) == 0) {
+    const ssize_t w = write(fd, out.data(), out.size());
+    (void)w;
+  }
+  return ok;
+}
 static std::mutex g_slot_mu;
 static int g_dedicated_slots[64] = {};
 static hipStream_t slot_stream(int dev, bool* dedicated) {
@@ -422,7 +476,7 @@ static hipStream_t slot_stream(int dev, bool* dedicated) {
     // (RT_SLOT_POOL, A/B knob: every slot on the runtime's pooled queues, as an ordinary stream)
     const char* pool_env = debug_env("RT_SLOT_POOL");
     if (!(pool_env && atoi(pool_env)) && dev >= 0 && dev < 64 && g_dedicated_slots[dev] < kDedicatedSlotQueues &&
-        hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) {
+        hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 && hwq_registry(dev, 1)) {
       std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xFFFFFFFFu);
       if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
         g_dedicated_slots[dev]++;
@@ -430,6 +484,7 @@ static hipStream_t slot_stream(int dev, bool* dedicated) {
         return st;
       }
       (void)hipGetLastError();
+      (void)hwq_registry(dev, -1);
       st = nullptr;
     }
   }
@@ -441,6 +496,7 @@ static void release_slot_stream(int dev, void* st, bool dedicated) {
   if (dedicated && dev >= 0 && dev < 64) {
     std::lock_guard<std::mutex> lk(g_slot_mu);
     g_dedicated_slots[dev]--;
+    (void)hwq_registry(dev, -1);
   }
 }
 constexpr int kEventFrames = 128;
