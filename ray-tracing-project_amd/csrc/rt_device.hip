@@ -418,13 +418,12 @@ static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // 
 // frames in flight overlap; the cap is per process, so several renderer processes sharing one GPU each add up
 // to 8 -- the 4-ranks-on-one-GPU rehearsal with and without (RT_SLOT_POOL) is in profiles/ab/r06_slot_queues_ab.txt.
 constexpr int kDedicatedSlotQueues = 8;
-// The same cap across the processes that share a GPU (counted per process only, four renderer processes
-// on one GPU held 32 dedicated queues and ran 4.1x slower than with every slot on the pool --
-// profiles/ab/r06_slot_queues_ab.txt). A lock file per physical GPU (/tmp/rtamd_hwq_<PCI bus id>) lists
-// "pid count" of the processes holding dedicated slot queues on it; entries of processes that no longer exist are
-// dropped, and the file is removed when no holder is left. Without the file (no /tmp, another user's file) a
-// process keeps its own cap only.
-constexpr int kDedicatedSlotQueuesPerGpu = 8;
+// Across the processes that share a GPU (the cap was counted per process only; four renderer processes
+// on one GPU held 32 dedicated queues and ran 4.1x slower than with every slot on the pool, and a shared cap of 8
+// queues still halved them -- profiles/ab/r06_slot_queues_ab.txt), only one process per GPU holds dedicated slot
+// queues. A lock file per physical GPU (/tmp/rtamd_hwq_<PCI bus id>) lists "pid count" of the processes holding
+// them; entries of processes that no longer exist are dropped, and the file is removed when no holder is left.
+// Without the file (no /tmp, another user's file) a process keeps its own cap only.
 static bool hwq_registry(int dev, int delta) {
   char bus[64] = {0};
   if (hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, dev) != hipSuccess) { (void)hipGetLastError(); return delta < 0; }
@@ -452,7 +451,10 @@ static bool hwq_registry(int dev, int delta) {
     pos = e + 1;
   }
   bool ok = true;
-  if (delta > 0 && others + mine + delta > kDedicatedSlotQueuesPerGpu) ok = false;
+  // one process per GPU holds dedicated queues (the first to ask): every other renderer process on that GPU takes
+  // the pool. (RT_HWQ_GPU_CAP=N, A/B knob: instead grant while all processes together hold at most N.)
+  const char* cap_env = debug_env("RT_HWQ_GPU_CAP");
+  if (delta > 0 && (cap_env ? others + mine + delta > atol(cap_env) : others > 0)) ok = false;
   else mine = std::max(0L, mine + delta);
   if (mine > 0) out += std::to_string(me) + " " + std::to_string(mine) + "\n";
   if (out.empty()) {  // no holder left: leave nothing behind (a process waiting on the old file re-counts alone)

@@ -66,10 +66,10 @@ for s in $STEPS; do
       # frame-slot streams on dedicated hardware queues (default) vs the runtime's pool (RT_SLOT_POOL=1): 2 and 4
       # torchrun ranks sharing the box's GPU (gloo timing reductions), and the single-process C3 / C5 lines
       export RTAMD_DEBUG_KNOBS=1
-      for rep in 1 2; do
-        for pool in 0 1; do
+      for rep in ${SLOTQ_REPS:-1 2}; do
+        for pool in ${SLOTQ_POOLS:-0 1}; do
           for n in 2 4; do
-            RT_SLOT_POOL=$pool BENCH_DEVICE=0 BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+            RT_HWQ_GPU_CAP=${HWQCAP:-8} RT_SLOT_POOL=$pool BENCH_DEVICE=0 BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
                 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n + 10 * pool)) bench.py --gpus $n \
                 --steps 20 --warmup 5 --no-cpu --no-e2e > $OUT/slotq_n${n}_p${pool}_r$rep.json 2> $OUT/slotq_n${n}_p${pool}_r$rep.err
             rc=$?; [ $rc -ne 0 ] && { echo "slotq n$n pool$pool rc=$rc"; tail -5 $OUT/slotq_n${n}_p${pool}_r$rep.err; hard $rc; exit $rc; }
