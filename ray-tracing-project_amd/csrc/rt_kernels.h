@@ -1254,6 +1254,17 @@ __device__ __forceinline__ Ray primary_ray(const FrameParams& P, int px, int py)
 // when off). HW_ID / XCC_ID via s_getreg (hwreg ids 4 and 20, all 32 bits).
 // The start clocks go to the wave's LDS words rather than staying live in registers for the whole
 // kernel (the FULL megakernel's allocation tips into heavy spilling otherwise).
+// A kernel argument read at this point of the kernel: the offset passes through an empty asm, so the load
+// cannot be hoisted to the kernel's start and its value is not held in registers before it is needed
+template <typename T>
+__device__ __forceinline__ T late_kernarg(size_t off) {
+  uint32_t o = (uint32_t)off;
+  asm volatile("" : "+s"(o));
+  typedef const __attribute__((address_space(4))) char* KArg;
+  const KArg base = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(base + o);
+}
+
 __device__ __forceinline__ void wave_clock_start(const FrameParams& P, uint32_t* clk) {
   if (P.timeline || P.cost) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -1279,23 +1290,28 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
   // split waves far above the rest and coarsens the order's buckets, -20% on C5 lone frames; keeping the
   // stale cost is within 1% of the maximum but never refreshes it; running cost-recording frames unsplit
   // costs 6%)
-  if (P.cost) {
+  if (P.cost && lane == 0) {
     const uint64_t dt = t1 - w.t0;
     const uint32_t c = dt > 0x3FFFFFFFull ? 0x3FFFFFFFu : (uint32_t)dt;
-    if (lane == 0) {
-      if (!sub_wave) P.cost[qw] = c;
-      else atomicMax(P.cost + qw, c);
-    }
-    // a moving camera: lane i < (2r + 1)^2 raises the map at the wave's i-th neighbour (whole frames: tile qw / 4
-    // sits at (tile % tiles_x, tile / tiles_x), its quarters 2 x 2 waves)
-    if (P.cost_dil) {
-      const int r = P.dil_r, d = 2 * r + 1;
-      if (lane < d * d) {
-        const int t = qw >> 2, q = qw & 3;
-        const int x = (t % P.tiles_x) * 2 + (q & 1) + lane % d - r, y = (t / P.tiles_x) * 2 + (q >> 1) + lane / d - r;
-        if (x >= 0 && y >= 0 && x < 2 * P.tiles_x && y < 2 * P.tiles_y)
-          atomicMax(P.cost_dil + 4 * ((y >> 1) * P.tiles_x + (x >> 1)) + (y & 1) * 2 + (x & 1), c);
-      }
+    if (!sub_wave) P.cost[qw] = c;
+    else atomicMax(P.cost + qw, c);
+  }
+  // a moving camera: lane i < (2r + 1)^2 raises the map at the wave's i-th neighbour (whole frames: tile qw / 4
+  // sits at (tile % tiles_x, tile / tiles_x), its quarters 2 x 2 waves). The fields are read here, from the
+  // kernel arguments (late_kernarg), so nothing of this stays live through the traversal: read through P, the
+  // compiler loaded them at the kernel's start and held them in SGPRs, spilling more of the kernel's SGPRs to
+  // VGPR lanes (C2 with frames in flight -4..-8%, round 6)
+  uint32_t* const dil = late_kernarg<uint32_t*>(offsetof(FrameParams, cost_dil));
+  if (dil) {
+    const uint64_t dt = t1 - w.t0;
+    const uint32_t c = dt > 0x3FFFFFFFull ? 0x3FFFFFFFu : (uint32_t)dt;
+    const int r = late_kernarg<int32_t>(offsetof(FrameParams, dil_r)), d = 2 * r + 1;
+    const int tx = late_kernarg<int32_t>(offsetof(FrameParams, tiles_x)), ty = late_kernarg<int32_t>(offsetof(FrameParams, tiles_y));
+    if (lane < d * d) {
+      const int t = qw >> 2, q = qw & 3;
+      const int x = (t % tx) * 2 + (q & 1) + lane % d - r, y = (t / tx) * 2 + (q >> 1) + lane / d - r;
+      if (x >= 0 && y >= 0 && x < 2 * tx && y < 2 * ty)
+        atomicMax(dil + 4 * ((y >> 1) * tx + (x >> 1)) + (y & 1) * 2 + (x & 1), c);
     }
   }
   if (!P.timeline) return;

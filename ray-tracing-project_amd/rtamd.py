@@ -155,8 +155,10 @@ def lib():
             L.rt_debug_env_knobs(1)
         L.rt_debug_timeline.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_debug_counters.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
-        if hasattr(L, "rt_debug_lpt_stats"):  # (API 4 libraries of round 5, loaded for A/B, lack these)
+        # (earlier API 4 builds, loaded for A/B through RTAMD_LIB, lack these)
+        if hasattr(L, "rt_debug_lpt_stats"):
             L.rt_debug_lpt_stats.argtypes = [vp, C.POINTER(C.c_int64)]
+        if hasattr(L, "rt_debug_wave_stats"):
             L.rt_debug_wave_stats.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int64)]
         L.rt_scene_save.argtypes = [vp, C.c_char_p]
         L.rt_frame_download_rgb8.argtypes = [vp, C.c_int64, vp, C.POINTER(C.c_int32)]
