@@ -709,7 +709,6 @@ void device_release(rt_scene* s) {
   if (s->lpt.d_cost) (void)hipFree(s->lpt.d_cost);
   if (s->lpt.d_cost_dil) (void)hipFree(s->lpt.d_cost_dil);
   if (s->lpt.d_order) (void)hipFree(s->lpt.d_order);
-  if (s->lpt.sort_done) (void)hipEventDestroy((hipEvent_t)s->lpt.sort_done);
   s->lpt = rt_scene::LptMap{};
   for (void* e : s->ev_pool) (void)hipEventDestroy((hipEvent_t)e);
   s->ev_pool.clear();
@@ -1318,14 +1317,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       HIPCHECK(hipMemsetAsync(lm.d_cost_dil, 0, waves * 4, st));
       lm.waves = waves;
     }
-    if (!lm.sort_done) {
-      hipEvent_t e;
-      HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      lm.sort_done = e;
-    }
-    // the previous lone frame's sort (queued after its frame-done event, on its own stream) may still be running:
-    // this frame reads its order and may overwrite the costs it reads, so its stream waits for it
-    HIPCHECK(hipStreamWaitEvent(st, (hipEvent_t)lm.sort_done, 0));
+
     const int64_t key[8] = {fr->width, fr->height, si, sc, fr->mode, depth0, P.xcd_remap, (int64_t)waves};
     const bool same = lm.valid && memcmp(key, lm.key, sizeof key) == 0;
     if (same) P.order = lm.d_order;
@@ -1478,20 +1470,19 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
   } else {
     HIPCHECK(hipEventRecord(ev_m, st));
   }
-  // the frame is done at ev_b; the sort for the scene's next lone frame of this shape follows it on the same
-  // stream, so rt_synchronize (which waits for ev_b) returns without it and the sort overlaps the caller's turn
-  // between two frames (the next lone frame waits for sort_done)
-  HIPCHECK(hipEventRecord(ev_b, st));
-  slot.last_done = ev_b;
+  // the sort for the scene's next lone frame of this shape, on this frame's stream before its done event: the next
+  // lone frame is queued only once every other slot's done event has passed (`alone`), so it finds the order
+  // complete whichever slot it takes
   if (lpt_sort) {
     uint32_t* in = lpt_dilate ? lm.d_cost_dil : lm.d_cost;
     hipLaunchKernelGGL(k_order_lpt, dim3(8), dim3(kLptThreads), 0, st, in, lpt_dilate ? lm.d_cost : (uint32_t*)nullptr,
                        lm.d_order, (int)units, P.xcd_remap, (variant & 262144) ? 1 : 0);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipEventRecord((hipEvent_t)lm.sort_done, st));
     lm.valid = true;
     lm.age = 0;
   }
+  HIPCHECK(hipEventRecord(ev_b, st));
+  slot.last_done = ev_b;
   s->last_slot = slot_id;
   s->next_slot = (slot_id + 1) % s->n_slots;
   s->last_W = fr->width;
@@ -1536,11 +1527,10 @@ static int check_prefetch_word(rt_scene* s) {
 static int sync_one(rt_scene* s, rt_stats* out) {
   int rc = check_device_scene(s);
   if (rc) return rc;
-  // every frame since the last synchronize has finished: each slot's latest frame-done event (a slot's frames
-  // run in order on its stream); the longest-first sort queued behind a lone frame may still run (its own event)
-  for (int k = 0; k < s->n_slots; k++) {
-    if (s->slots[k].last_done) HIPCHECK(hipEventSynchronize((hipEvent_t)s->slots[k].last_done));
-  }
+  // every slot's stream drained. (Round 6 tried waiting for each slot's frame-done event only, so that a lone
+  // frame's trailing sort could overlap the caller's turn: the same frames with 4 in flight then ran 4-25% slower
+  // from one process to the next -- C2 29.8-35.0 against 37.6-38.5 Grays/s, profiles/ab/r06_sync_ab.txt.)
+  for (int k = 0; k < s->n_slots; k++) HIPCHECK(hipStreamSynchronize((hipStream_t)s->slots[k].stream));
   if ((rc = check_prefetch_word(s))) return rc;
   struct Reset {
     rt_scene* s;

@@ -89,6 +89,22 @@ for s in $STEPS; do
       # the drop-in CLI (host/main.cpp) on the C3 scene: scene setup time with the library default builders
       timeout -k 10 300 python tools/cli_c3.py > $OUT/cli_c3.json 2> $OUT/cli_c3.err
       rc=$?; echo "cli rc=$rc"; cat $OUT/cli_c3.json; hard $rc ;;
+    c2diag)
+      # C2 (bunny PRIMARY, 4 frames in flight) run to run: the library as built, the round-5 per-process queue cap
+      # (RT_HWQ_GPU_CAP=1000), every slot on the pool (RT_SLOT_POOL=1); fresh process each
+      export RTAMD_DEBUG_KNOBS=1
+      for rep in 1 2 3; do
+        for v in ${C2V:-lib cap1000 pool}; do
+          case $v in lib) envs="";; cap1000) envs="RT_HWQ_GPU_CAP=1000";; pool) envs="RT_SLOT_POOL=1";;
+                     ss) envs="RT_SYNC_STREAMS=1";; sb) envs="RT_SORT_BEFORE=1";; both) envs="RT_SYNC_STREAMS=1 RT_SORT_BEFORE=1";;
+                     r06a) envs="RTAMD_LIB=$PWD/ray-tracing-project_amd/lib/librtamd_r06a.so";; esac
+          env $envs timeout -k 10 120 python bench.py --scene bunny --mode primary --steps 40 --warmup 5 --no-cpu --no-side \
+              --no-extra --no-e2e --no-stats --no-cold --no-moving > $OUT/c2diag_${v}_r$rep.json 2> $OUT/c2diag_${v}_r$rep.err
+          rc=$?; [ $rc -ne 0 ] && { echo "c2diag $v rc=$rc"; hard $rc; exit $rc; }
+          python3 -c "import json;d=json.loads(open('$OUT/c2diag_${v}_r$rep.json').read().strip().splitlines()[-1]);c=d['config'];print('c2diag $v r$rep', d['value'], d['ms_per_step'], c['kernel_ms_one_frame_alone'], c['kernel_ms_per_frame'])"
+        done
+      done
+      unset RTAMD_DEBUG_KNOBS ;;
     hybrid)
       # the counting run's packet -> per-lane hybrid model (C3 soup, C2 bunny)
       timeout -k 10 300 python tools/hybrid_model.py soup bunny > $OUT/hybrid_model.jsonl 2> $OUT/hybrid_model.err
