@@ -1310,8 +1310,11 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
     if (lane < d * d) {
       const int t = qw >> 2, q = qw & 3;
       const int x = (t % tx) * 2 + (q & 1) + lane % d - r, y = (t / tx) * 2 + (q >> 1) + lane / d - r;
+      // the wave itself raises its own slot by its cost, its neighbours by 3/4 of it: where the camera stands still
+      // the costliest waves still rank first (and take the split), where it moves their neighbours rank next
+      const uint32_t v = lane == (d * d) / 2 ? c : c - (c >> 2);
       if (x >= 0 && y >= 0 && x < 2 * tx && y < 2 * ty)
-        atomicMax(dil + 4 * ((y >> 1) * tx + (x >> 1)) + (y & 1) * 2 + (x & 1), c);
+        atomicMax(dil + 4 * ((y >> 1) * tx + (x >> 1)) + (y & 1) * 2 + (x & 1), v);
     }
   }
   if (!P.timeline) return;

@@ -46,12 +46,17 @@ for fif in (1, 4):
         sc.render_async(static, rt.DEFAULT_LIGHTS, W, H, mode=m)
         sc.synchronize()
     for rep in range(reps):
-        for cam_kind in ("static", "moving"):
-            path = rt.CameraPath(W, H) if cam_kind == "moving" else None
-            for _ in range(10):  # the path's first poses (untimed)
+        for cam_kind in ("static", "moving", "stopped"):
+            # stopped: 20 untimed moving frames, then the timed frames hold the path's last pose (the camera stops)
+            path = rt.CameraPath(W, H) if cam_kind != "static" else None
+            for _ in range(10 if cam_kind != "stopped" else 20):  # the path's first poses (untimed)
                 sc.render_async(path.next() if path else static, rt.DEFAULT_LIGHTS, W, H, mode=m)
                 sc.synchronize()
-            cams = path.take(frames) if path else [static] * frames
+            if cam_kind == "stopped":
+                hold = path.camera()
+                cams = [hold] * frames
+            else:
+                cams = path.take(frames) if path else [static] * frames
             k_ms = tr_ms = el = 0.0
             torch.cuda.synchronize()
             for c in cams:
