@@ -1343,7 +1343,9 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     // refresh and spend no sort per frame. (RT_LPT_MOVED forces either rule.)
     const bool l2_small = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
     const bool resort_on_motion = moved_env ? key_moved : (key_moved && l2_small);
-    lpt_sort = !same || ++lm.age >= refresh || (resort_on_motion && moved);
+    // (a dilated map is replaced by the first frame after the camera stopped: dilated, the map spends the split on
+    // the costly waves' neighbours -- 0.30 ms instead of 0.22 on C5 at an exact pose)
+    lpt_sort = !same || ++lm.age >= refresh || (resort_on_motion && moved) || (lm.dilated_map && !moving);
     lm.frames++;
     if (lpt_sort) {
       memcpy(lm.key, key, sizeof key);
@@ -1354,6 +1356,7 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       const char* dil_env = debug_env("RT_LPT_DILATE");
       const int r = dil_env ? std::max(0, std::min(4, atoi(dil_env))) : kLptDilate;
       lpt_dilate = (moving && resort_on_motion && sc == 1 && !dual) ? r : 0;
+      lm.dilated_map = lpt_dilate > 0;
       if (lpt_dilate) {
         lm.dilated++;
         P.cost_dil = lm.d_cost_dil;

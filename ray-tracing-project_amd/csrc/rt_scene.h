@@ -234,6 +234,7 @@ struct rt_scene {
     float view[16] = {0};   // the camera of the frame whose costs made the order
     float prev_view[16] = {0};  // the camera of the scene's previous lone frame (motion test)
     uint32_t* d_cost_dil = nullptr;  // a moving camera's costs dilated over neighbouring waves (FrameParams::cost_dil)
+    bool dilated_map = false;        // the order was sorted from dilated costs
     int64_t sorts = 0, frames = 0, dilated = 0;  // lone frames dispatched longest-first / that re-sorted / dilated
   } lpt;
   static constexpr int kMaxSlots = 4;
