@@ -112,6 +112,33 @@ def test_camera_path_matches_flycam(rt, dxyz):
     assert len({tuple(x) for x in t}) > 100
 
 
+def test_moving_pose_fixture_matches_bench():
+    """The committed moving-camera digests (tools/gen_fullframe_digests.py) are of the pose bench.py and the GPU
+    test check: the same MOVE_POSE, and the fixture records the view translation that pose has."""
+    import importlib.util
+    import json
+
+    def load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        return m
+    bench = load("bench_mp", os.path.join(ROOT, "bench.py"))
+    gen = load("gen_mp", os.path.join(ROOT, "tools", "gen_fullframe_digests.py"))
+    src = open(os.path.join(ROOT, "tests", "test_gpu_fullframe.py")).read()
+    assert bench.MOVE_POSE == gen.MOVE_POSE and f"MOVE_POSE = {bench.MOVE_POSE}" in src
+    dig = json.load(open(os.path.join(GOLDEN, "fullframe_digests.json")))
+    import importlib
+    rt = importlib.import_module("conftest").rtamd
+    for case in ("C3-moving", "C5-moving"):
+        d = dig[case]
+        assert d["camera_path_pose"] == bench.MOVE_POSE
+        p = rt.CameraPath(d["W"], d["H"])
+        p.take(bench.MOVE_POSE)
+        c = p.camera()
+        assert [c.view_matrix[12], c.view_matrix[13], c.view_matrix[14]] == d["view_translation"]
+
+
 @pytest.mark.parametrize("sec", read_kat(), ids=lambda s: f"op{s[0]}")
 def test_host_math_matches_eigen(rt, sec):
     op, n, il, ol, inp, exp = sec
