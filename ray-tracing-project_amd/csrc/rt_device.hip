@@ -415,8 +415,8 @@ static size_t alloc_bytes(size_t bytes) { return bytes == 0 ? 16 : bytes; }  // 
 // (32 dedicated queues) ran 2.3x slower than two (profiles/ab/r05_queue_probe.txt) -- so further slots take the
 // pool. dedicated_slots counts the live dedicated queues per device (released by release_slot_stream).
 // A deliberate exception to the per-process GPU_MAX_HW_QUEUES pool: it is what lets one process's
-// frames in flight overlap; the cap is per process, so several renderer processes sharing one GPU each add up
-// to 8 -- the 4-ranks-on-one-GPU rehearsal with and without (RT_SLOT_POOL) is in profiles/ab/r06_slot_queues_ab.txt.
+// frames in flight overlap (C5 with 4 frames in flight 11.9 against 8.6 Grays/s on the pool); RT_SLOT_POOL (A/B
+// knob) puts every slot on the pool.
 constexpr int kDedicatedSlotQueues = 8;
 // Across the processes that share a GPU (the cap was counted per process only; four renderer processes
 // on one GPU held 32 dedicated queues and ran 4.1x slower than with every slot on the pool, and a shared cap of 8

@@ -85,6 +85,13 @@ for s in $STEPS; do
         done
       done
       unset RTAMD_DEBUG_KNOBS ;;
+    rehearse8)
+      # the driver's 8-GPU launch rehearsed on the box's one GPU: torchrun 8 ranks (gloo timing reductions), the
+      # scene built once by rank 0 and loaded by the others, cold + prewarmed C4 shards, e2e frame over gloo
+      BENCH_DEVICE=0 BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+          --master-addr 127.0.0.1 --master-port 29788 bench.py --gpus 8 --steps 20 --warmup 5 --no-cpu \
+          > $OUT/rehearse8.json 2> $OUT/rehearse8.err
+      rc=$?; echo "rehearse8 rc=$rc"; cat $OUT/rehearse8.json; hard $rc ;;
     cli)
       # the drop-in CLI (host/main.cpp) on the C3 scene: scene setup time with the library default builders
       timeout -k 10 300 python tools/cli_c3.py > $OUT/cli_c3.json 2> $OUT/cli_c3.err
