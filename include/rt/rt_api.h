@@ -440,7 +440,7 @@ int rt_debug_scene_flags(const rt_scene* s, int64_t counts[3], float* cert_origi
 int rt_debug_set_variant(int32_t v);
 /* Diagnostics: on = 1 lets the library read its A/B and diagnostic environment knobs (RT_KERNEL_VARIANT,
  * RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_TIMELINE_SPLIT, RT_XCD_RUN, RT_LDS_PAD, RT_LPT_REFRESH, RT_LPT_MOVED,
- * RT_LPT_DILATE, RT_ASM_DEVICE, RT_SLOT_POOL, RT_HWQ_GPU_CAP, RT_SAH_TRAV, RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING); by default
+ * RT_LPT_DILATE, RT_LPT_PRED, RT_LPT_DILW, RT_ASM_DEVICE, RT_SLOT_POOL, RT_HWQ_GPU_CAP, RT_SAH_TRAV, RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING); by default
  * (and after on = 0) it ignores the process environment, so a drop-in's trees, kernels and dispatch never
  * depend on it. Turning it on also takes RT_KERNEL_VARIANT as the current kernel variant. */
 int rt_debug_env_knobs(int32_t on);

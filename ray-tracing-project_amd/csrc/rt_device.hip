@@ -37,6 +37,40 @@ namespace rt {
 constexpr int kLptBuckets = 32, kLptThreads = 512, kLptRefresh = 8;
 constexpr bool kLptMoved = true;  // re-sort after every lone frame whose camera moved since the map's frame
 constexpr int kLptDilate = 2;     // a moving camera's map: each wave's cost = the max over (2r+1)^2 waves around it
+// ... or around the waves where its content is expected next frame (FrameParams::pred), then over a ring of 1
+// (profiles/ab/r06_moving_prediction_ab.txt: C5 moving lone frames 0.295 -> 0.26 ms)
+constexpr bool kLptPred = true;
+constexpr int kLptDilatePred = 1;
+
+// The camera's last step as a view-space transform, D = V_n V_(n-1)^-1 (both world -> view, column-major 4 x 4
+// affine, tucano Camera::view_matrix); its translation (FrameParams::pred_step). Flycamera::translate (the
+// reference's WASD keys, flycamera.hpp:196-202) moves translation_vector under a fixed rotation, so D is a pure
+// translation there; a rotated step keeps only its translation (the prediction is a dispatch-order hint).
+static void camera_step(const float* vp_prev, const float* v_cur, float* step3) {
+  double R[3][3], t[3], Ri[3][3];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) R[i][j] = vp_prev[4 * j + i];
+    t[i] = vp_prev[12 + i];
+  }
+  const double det = R[0][0] * (R[1][1] * R[2][2] - R[1][2] * R[2][1]) - R[0][1] * (R[1][0] * R[2][2] - R[1][2] * R[2][0]) +
+                     R[0][2] * (R[1][0] * R[2][1] - R[1][1] * R[2][0]);
+  step3[0] = step3[1] = step3[2] = 0.0f;
+  if (!(std::fabs(det) > 1e-30)) return;  // degenerate previous view: no step
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      const int a = (j + 1) % 3, b = (j + 2) % 3, c = (i + 1) % 3, d = (i + 2) % 3;
+      Ri[i][j] = (R[a][c] * R[b][d] - R[a][d] * R[b][c]) / det;  // inverse = adjugate / det
+    }
+  for (int i = 0; i < 3; i++) {  // D's translation: t_n - R_n R_(n-1)^-1 t_(n-1)
+    double m = v_cur[12 + i];
+    for (int j = 0; j < 3; j++) {
+      double rr = 0.0;
+      for (int k = 0; k < 3; k++) rr += (double)v_cur[4 * k + i] * Ri[k][j];
+      m -= rr * t[j];
+    }
+    step3[i] = (float)m;
+  }
+}
 constexpr int kSplitK = 1536;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k); round 5
                                // re-sweep without the spill: 1536 +2.5..6% over 2048 (profiles/ab/r05_c5_split_ab.txt)
 constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
@@ -1331,16 +1365,21 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
     const int refresh = refresh_env ? std::max(1, atoi(refresh_env)) : kLptRefresh;
     const bool key_moved = moved_env ? atoi(moved_env) != 0 : kLptMoved;
     const bool moved = memcmp(cam->view_matrix, lm.view, sizeof lm.view) != 0;
-    // moving: this frame's camera differs from the previous lone frame's -> its costs are dilated before the sort
-    // (whole frames only: the wave grid of a shard is not contiguous). RT_LPT_DILATE: A/B knob (radius, 0 = off)
+    // moving: this frame's camera differs from the previous lone frame's -> its costs are placed where each wave's
+    // content is expected in the next frame (the camera repeating its step, FrameParams::pred) and dilated before the
+    // sort (whole frames only: the wave grid of a shard is not contiguous). RT_LPT_DILATE / RT_LPT_PRED: A/B knobs
     const bool moving = memcmp(cam->view_matrix, lm.prev_view, sizeof lm.prev_view) != 0;
+    float prev_view[16];
+    memcpy(prev_view, lm.prev_view, sizeof prev_view);
     memcpy(lm.prev_view, cam->view_matrix, sizeof lm.prev_view);
     // Measured under the reference's moving camera (profiles/ab/r06_moving_camera_ab.txt, one frame at a time):
     // an L2-resident scene whose lone frames split their costliest waves (C5: the bunny's silhouette tiles) loses
     // the split's gain with a map even one frame old (0.38 ms against 0.227 with an exact map) and regains most
-    // of it with a fresh, dilated map (0.31 ms); the soup's per-wave costs decorrelate within a frame of motion
-    // (fresh or 8 frames old, dilated or not: 0.233-0.237 ms, no map 0.245), so large scenes keep the 8-frame
-    // refresh and spend no sort per frame. (RT_LPT_MOVED forces either rule.)
+    // of it with a fresh, dilated map (0.31 ms), more with the costs moved to their predicted waves (0.26 ms,
+    // profiles/ab/r06_moving_prediction_ab.txt); the soup's per-wave costs decorrelate within a frame of motion
+    // (fresh or 8 frames old, dilated or not: 0.233-0.237 ms, no map 0.245; predicted: 0.226 ms, but the sort on
+    // every frame's path takes it back), so large scenes keep the 8-frame refresh and spend no sort per frame.
+    // (RT_LPT_MOVED forces either rule.)
     const bool l2_small = (s->hs.nodes.size() + s->hs.tris.size()) * 64 <= kFullSmallSceneBytes;
     const bool resort_on_motion = moved_env ? key_moved : (key_moved && l2_small);
     // (a dilated map is replaced by the first frame after the camera stopped: dilated, the map spends the split on
@@ -1353,14 +1392,29 @@ static int render_one(rt_scene* s, const rt_camera* cam, const rt_light* lights,
       lm.valid = false;  // until this frame's k_order_lpt has been queued
       P.cost = lm.d_cost;
       lm.sorts++;
-      const char* dil_env = debug_env("RT_LPT_DILATE");
-      const int r = dil_env ? std::max(0, std::min(4, atoi(dil_env))) : kLptDilate;
-      lpt_dilate = (moving && resort_on_motion && sc == 1 && !dual) ? r : 0;
-      lm.dilated_map = lpt_dilate > 0;
-      if (lpt_dilate) {
+      // RT_LPT_PRED (A/B knob): each wave's cost lands where its content is expected next frame (FrameParams::pred)
+      const char* pred_env = debug_env("RT_LPT_PRED");
+      const bool pred = pred_env ? atoi(pred_env) != 0 : kLptPred;
+      const char* dil_env = debug_env("RT_LPT_DILATE");  // (2 + 2 r)^2 <= 64 lanes
+      const int r = dil_env ? std::max(0, std::min(3, atoi(dil_env))) : (pred ? kLptDilatePred : kLptDilate);
+      const char* dilw_env = debug_env("RT_LPT_DILW");  // A/B knob: the ring's weight 1 - 2^-w (default 3/4)
+      const int dil_w = dilw_env ? std::max(1, std::min(8, atoi(dilw_env))) : 2;
+      const bool moving_map = moving && resort_on_motion && sc == 1 && !dual && (r > 0 || pred);
+      lpt_dilate = moving_map;
+      lm.dilated_map = moving_map;
+      if (moving_map) {
         lm.dilated++;
         P.cost_dil = lm.d_cost_dil;
-        P.dil_r = lpt_dilate;
+        P.dil_r = r;
+        P.dil_w = dil_w;
+        if (pred) {  // a pixel's view-space direction (nx xscale, ny yscale, -1) as (a px + b, c py + e, -1)
+          P.pred = 1;
+          P.pred_proj[0] = 2.0f * P.xscale / P.vp[2];
+          P.pred_proj[1] = -(2.0f * P.vp[0] / P.vp[2] + 1.0f) * P.xscale;
+          P.pred_proj[2] = -2.0f * P.yscale / P.vp[3];
+          P.pred_proj[3] = (1.0f + 2.0f * P.vp[1] / P.vp[3]) * P.yscale;
+          camera_step(prev_view, cam->view_matrix, P.pred_step);
+        }
       }
     }
   }

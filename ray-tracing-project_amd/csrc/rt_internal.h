@@ -244,6 +244,14 @@ struct FrameParams {
   // wave's neighbourhood maximum; null = off
   uint32_t* cost_dil;
   int32_t dil_r;
+  int32_t dil_w;  // the ring's cost = cost - (cost >> dil_w)
+  // pred: each wave raises cost_dil around the wave where its primary hit point is expected in the next frame
+  // instead of around itself (rt_kernels.h pred_mark / wave_clock_end): pred_proj = (a, b, c, e), a pixel's
+  // view-space ray direction (a px + b, c py + e, -1); pred_step = the camera's last step as a view-space
+  // translation (V_n V_(n-1)^-1), applied once more; 0 = off
+  int32_t pred;
+  float pred_proj[4];
+  float pred_step[3];
   // RT_FRAME_WAVE_STATS (a counting frame, diagnostics): 8 words per logical wave (rt_debug_wave_stats)
   uint32_t* wave_stats;
   // k_render_full with an order: the first split_k logical waves of the order (the costliest of an

@@ -1276,8 +1276,11 @@ __device__ __forceinline__ void wave_clock_start(const FrameParams& P, uint32_t*
     }
   }
 }
+// tprim (PRIMARY / FULL frame kernels): each lane's primary hit distance (INFINITY: missed or inactive), stored to
+// LDS right after the primary hit -- one ds_write per lane, no branch, nothing held in registers -- for a moving
+// camera's prediction below (FrameParams::pred)
 __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint32_t* clk, int lane, int qw,
-                                               bool sub_wave = false) {
+                                               bool sub_wave = false, const float* tprim = nullptr) {
   if (!P.timeline && !P.cost) return;
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   struct { uint64_t t0; uint32_t r0; } w;
@@ -1296,7 +1299,7 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
     if (!sub_wave) P.cost[qw] = c;
     else atomicMax(P.cost + qw, c);
   }
-  // a moving camera: lane i < (2r + 1)^2 raises the map at the wave's i-th neighbour (whole frames: tile qw / 4
+  // a moving camera: lane i raises the map at the i-th wave around the wave's footprint (whole frames: tile qw / 4
   // sits at (tile % tiles_x, tile / tiles_x), its quarters 2 x 2 waves). The fields are read here, from the
   // kernel arguments (late_kernarg), so nothing of this stays live through the traversal: read through P, the
   // compiler loaded them at the kernel's start and held them in SGPRs, spilling more of the kernel's SGPRs to
@@ -1305,14 +1308,46 @@ __device__ __forceinline__ void wave_clock_end(const FrameParams& P, const uint3
   if (dil) {
     const uint64_t dt = t1 - w.t0;
     const uint32_t c = dt > 0x3FFFFFFFull ? 0x3FFFFFFFu : (uint32_t)dt;
-    const int r = late_kernarg<int32_t>(offsetof(FrameParams, dil_r)), d = 2 * r + 1;
+    const int r = late_kernarg<int32_t>(offsetof(FrameParams, dil_r));
     const int tx = late_kernarg<int32_t>(offsetof(FrameParams, tiles_x)), ty = late_kernarg<int32_t>(offsetof(FrameParams, tiles_y));
-    if (lane < d * d) {
-      const int t = qw >> 2, q = qw & 3;
-      const int x = (t % tx) * 2 + (q & 1) + lane % d - r, y = (t / tx) * 2 + (q >> 1) + lane / d - r;
-      // the wave itself raises its own slot by its cost, its neighbours by 3/4 of it: where the camera stands still
-      // the costliest waves still rank first (and take the split), where it moves their neighbours rank next
-      const uint32_t v = lane == (d * d) / 2 ? c : c - (c >> 2);
+    const int t = qw >> 2, q = qw & 3;
+    // the wave's pixel origin: its own, or where a moving camera's prediction (FrameParams::pred) expects its
+    // content in the next frame -- one hit lane's primary hit (lane 36, the wave's centre, when it hit, else the
+    // first hit lane): t along its view-space direction (a px + b, c py + e, -1) (the camera is rigid, so t is a
+    // view-space distance), moved by the camera's last step (pred_step: a translation in view space, as the
+    // reference's WASD keys make it) and projected back to a pixel; its own when no lane hit
+    float ox = (float)(((t % tx) * 2 + (q & 1)) * 8), oy = (float)(((t / tx) * 2 + (q >> 1)) * 8);
+    const uint64_t hb = (tprim && late_kernarg<int32_t>(offsetof(FrameParams, pred)))
+                            ? ballot(reinterpret_cast<const volatile float*>(tprim)[lane] != INFINITY) : 0;
+    if (hb != 0) {
+      const int rep = ((hb >> 36) & 1) ? 36 : (int)__builtin_ctzll(hb);
+      const float th = reinterpret_cast<const volatile float*>(tprim)[rep];
+      const size_t po = offsetof(FrameParams, pred_proj), so = offsetof(FrameParams, pred_step);
+      const float a = late_kernarg<float>(po), b = late_kernarg<float>(po + 4), cc = late_kernarg<float>(po + 8),
+                  e = late_kernarg<float>(po + 12);
+      const float dx = a * (ox + (float)(rep & 7)) + b, dy = cc * (oy + (float)(rep >> 3)) + e;
+      const float k = th / sqrtf(dx * dx + dy * dy + 1.0f);
+      const float qx = dx * k + late_kernarg<float>(so), qy = dy * k + late_kernarg<float>(so + 4),
+                  qz = late_kernarg<float>(so + 8) - k;
+      if (qz < 0.0f) {
+        const float sx = (qx / -qz - b) / a - (float)(rep & 7), sy = (qy / -qz - e) / cc - (float)(rep >> 3);
+        if (sx > -8.0f && sy > -8.0f && sx < 16.0f * (float)tx && sy < 16.0f * (float)ty) {
+          ox = sx;
+          oy = sy;
+        }
+      }
+    }
+    // the waves the 8 x 8 footprint at (ox, oy) overlaps (1 x 1 at the wave's own position, up to 2 x 2 when
+    // predicted) take its full cost, a ring of r waves around them 3/4 of it (dil_w: the ring's shift, 2 = 3/4, 1 =
+    // 1/2): where the camera stands still the costliest waves still rank first (and take the split), where it
+    // moves their neighbours rank next
+    const int x0 = (int)floorf(ox * 0.125f), y0 = (int)floorf(oy * 0.125f);
+    const int fw = ox * 0.125f != (float)x0 ? 2 : 1, fh = oy * 0.125f != (float)y0 ? 2 : 1;
+    const int dw = fw + 2 * r, dh = fh + 2 * r;
+    if (lane < dw * dh) {
+      const int i = lane % dw, j = lane / dw, x = x0 - r + i, y = y0 - r + j;
+      const bool inner = i >= r && i < r + fw && j >= r && j < r + fh;
+      const uint32_t v = inner ? c : c - (c >> late_kernarg<int32_t>(offsetof(FrameParams, dil_w)));
       if (x >= 0 && y >= 0 && x < 2 * tx && y < 2 * ty)
         atomicMax(dil + 4 * ((y >> 1) * tx + (x >> 1)) + (y & 1) * 2 + (x & 1), v);
     }
@@ -1446,6 +1481,7 @@ template <bool HITS, bool BOXCOL = false>
 __global__ __launch_bounds__(64 * kTraceWPB) __attribute__((amdgpu_waves_per_eu(kTraceWavesPerEu)))
 void k_primary_fused(FrameParams P) {
   __shared__ WaveLds<TRAV_B2_LDS, false> lds;
+  __shared__ float tprim[64];  // the lanes' primary hit distances (wave_clock_end's prediction)
   wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<kTraceWPB>(P);
   // the eye (every primary ray's origin) held in VGPRs: origin.dot(facenormal) in each triangle test
@@ -1454,8 +1490,9 @@ void k_primary_fused(FrameParams P) {
   asm("" : "+v"(r.o.x), "+v"(r.o.y), "+v"(r.o.z));
   Hit h{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   trace_closest_oct<false, TRAV_B2_LDS, true>(P.sc, r, c.active, h, lds, c.slot, nullptr);
+  tprim[c.lane] = h.t;  // (INFINITY for a miss or an inactive lane)
   if (c.active) shade_primary_pixel<HITS, BOXCOL>(P, r, (size_t)c.py * P.W + c.px, h.t, h.slot);
-  wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0);
+  wave_clock_end(P, lds.clk, c.lane, c.qw, c.sub >= 0, tprim);
 }
 
 // FULL: the reference traceRay as-is (max_depth 2): shadow any-hit per light and one reflection
@@ -1490,7 +1527,7 @@ __device__ __forceinline__ void phase_end(uint32_t* cnt, int p, const PhaseMark&
 
 template <bool STATS, int TRAV, bool SPLIT = false>
 __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, bool active, WaveLds<TRAV, STATS>& lds, int wv,
-                                         uint32_t* cnt, Hit& h, uint32_t& face0) {
+                                         uint32_t* cnt, Hit& h, uint32_t& face0, float* tprim = nullptr) {
   h = Hit{INFINITY, 0xFFFFFFFFu, 0xFFFFFFFFu};
   bool dummy = false;
   // the primary packet is coherent: octant-specialised loops
@@ -1499,6 +1536,7 @@ __device__ __forceinline__ f3 trace_full(const FrameParams& P, const Ray& r, boo
   phase_end<STATS>(cnt, 0, pm, active);
   const bool hit0 = active && h.t != INFINITY;
   if (STATS && hit0) cnt[ST_HITS]++;
+  if (tprim) tprim[lane_id()] = hit0 ? h.t : INFINITY;
 
   MatState st = load_mat(P.defmat);
   HitInfo hi0;
@@ -1588,6 +1626,7 @@ void k_render_full(FrameParams P) {
   // spilled to scratch (16 B per lane written at every pixel: ~33 MB of HBM writes per 1080p frame
   // against the 24.9 MB frame itself)
   __shared__ uint32_t pix_xy[2][64];
+  __shared__ float tprim[64];  // the lanes' primary hit distances (wave_clock_end's prediction)
   wave_clock_start(P, lds.clk);
   const PixelCoord c = pixel_coord<kFullWPB>(P);
   const bool active = c.active;
@@ -1599,7 +1638,7 @@ void k_render_full(FrameParams P) {
 
   Hit h;
   uint32_t face0;
-  const f3 col = trace_full<STATS, TRAV, WPE == kFullWavesPerEuSmall>(P, r, active, lds, c.slot, cnt, h, face0);
+  const f3 col = trace_full<STATS, TRAV, WPE == kFullWavesPerEuSmall>(P, r, active, lds, c.slot, cnt, h, face0, tprim);
   const bool hit0 = face0 != 0xFFFFFFFFu;
   const uint32_t lane = lane_id_fresh();
   const uint32_t px = reinterpret_cast<volatile uint32_t*>(pix_xy[0])[lane];
@@ -1618,7 +1657,7 @@ void k_render_full(FrameParams P) {
     wave_stats_out(P, cnt, (int)lane, c.qw, true);
     flush_stats(P, cnt, (int)lane);
   }
-  wave_clock_end(P, lds.clk, (int)lane, c.qw, c.sub >= 0);
+  wave_clock_end(P, lds.clk, (int)lane, c.qw, c.sub >= 0, tprim);
 }
 
 // traceRay(o, d, 0) for any recursion limit D = P.max_depth (flyscene.cpp:317-371; the reference fixes

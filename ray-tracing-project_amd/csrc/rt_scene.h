@@ -107,7 +107,7 @@ float scene_static_pad(const HostScene& hs);
 float cert_origin_max(const HostScene& hs);
 uint32_t tri_flags(const HostScene& hs, uint32_t f, float Ro);  // kSafeNormalBit | kBoxCertBit of face f
 void set_error(const char* fmt, ...);
-// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_XCD_RUN, RT_LDS_PAD, RT_LPT_REFRESH, RT_LPT_MOVED, RT_LPT_DILATE, RT_ASM_DEVICE, RT_SLOT_POOL, RT_HWQ_GPU_CAP, RT_SAH_TRAV,
+// Diagnostic / A/B environment knobs (RT_KERNEL_VARIANT, RT_SPLIT_K, RT_SPLIT_KP, RT_SPLIT_KP_ANY, RT_XCD_RUN, RT_LDS_PAD, RT_LPT_REFRESH, RT_LPT_MOVED, RT_LPT_DILATE, RT_LPT_PRED, RT_LPT_DILW, RT_ASM_DEVICE, RT_SLOT_POOL, RT_HWQ_GPU_CAP, RT_SAH_TRAV,
 // RT_SBVH_BUDGET, RT_NODE_LAYOUT, RT_PLOC_RADIUS, RT_PLOC_TRAV, RT_PLOC_RULE, RT_TIMING): getenv(name) once rt_debug_env_knobs(1) has been called,
 // else nullptr -- the product library's behaviour never depends on the caller's environment otherwise.
 const char* debug_env(const char* name);

@@ -112,6 +112,46 @@ def test_camera_path_matches_flycam(rt, dxyz):
     assert len({tuple(x) for x in t}) > 100
 
 
+def test_moving_camera_prediction_geometry(rt):
+    """The moving camera's cost-map prediction (rt_kernels.h wave_clock_end, FrameParams::pred): a hit at distance t
+    along pixel (px, py)'s view-space direction (a px + b, c py + e, -1), moved by the camera's last step
+    (rt_device.hip camera_step: the translation of V_n V_(n-1)^-1) and projected back, lands on the pixel where the
+    same world point appears in the path's next frame. The same algebra as the kernel, in float64, against the
+    reference camera path's actual next pose (WASD translate, Flyscene::simulate)."""
+    W, H = 1920, 1080
+    cams = rt.CameraPath(W, H).take(30)
+
+    def V(c):
+        return np.array(c.view_matrix, np.float64).reshape(4, 4).T
+
+    def pixel(c, p):
+        q = V(c) @ np.append(p, 1.0)
+        xs, ys = c.aspect_ratio * np.tan(np.radians(c.fovy / 2)), np.tan(np.radians(c.fovy / 2))
+        nx, ny = (q[0] / -q[2]) / xs, (q[1] / -q[2]) / ys
+        return np.array([(nx + 1) / 2 * c.viewport[2] + c.viewport[0], (1 - ny) / 2 * c.viewport[3] + c.viewport[1]]), q
+
+    rng = np.random.default_rng(7)
+    for n in (1, 10, 24, 25, 26):  # frame 25 moves A after 25 frames of D: a one-frame miss of the prediction
+        prev, cur, nxt = cams[n - 1], cams[n], cams[n + 1]
+        xs, ys = cur.aspect_ratio * np.tan(np.radians(cur.fovy / 2)), np.tan(np.radians(cur.fovy / 2))
+        vp = np.array(cur.viewport, np.float64)
+        a, b = 2 * xs / vp[2], -(2 * vp[0] / vp[2] + 1) * xs
+        c, e = -2 * ys / vp[3], (1 + 2 * vp[1] / vp[3]) * ys
+        step = (V(cur) @ np.linalg.inv(V(prev)))[:3, 3]
+        for p in rng.uniform([-0.5, -0.5, -0.6], [0.5, 0.5, 0.2], (20, 3)):
+            (px, py), q = pixel(cur, p)
+            t = np.linalg.norm(q[:3])
+            dx, dy = a * px + b, c * py + e
+            k = t / np.sqrt(dx * dx + dy * dy + 1)
+            qx, qy, qz = dx * k + step[0], dy * k + step[1], step[2] - k
+            pred = np.array([(qx / -qz - b) / a, (qy / -qz - e) / c])
+            true, _ = pixel(nxt, p)
+            if n == 25:  # the step reverses: the prediction misses (by twice the x step)
+                assert np.abs(pred - true).max() > 1e-3
+            else:
+                assert np.abs(pred - true).max() < 1e-6
+
+
 def test_moving_pose_fixture_matches_bench():
     """The committed moving-camera digests (tools/gen_fullframe_digests.py) are of the pose bench.py and the GPU
     test check: the same MOVE_POSE, and the fixture records the view translation that pose has."""

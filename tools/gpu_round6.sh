@@ -32,13 +32,13 @@ for s in $STEPS; do
       # lone frames under the moving camera: this library's longest-first policies, and the round-5 library
       # (per-slot cost maps) when lib/librtamd_r05.so was built beside it (tools/moving_ab.py)
       export RTAMD_DEBUG_KNOBS=1
-      for sc in soup:primary bunny:full; do
+      for sc in ${MSCENES:-soup:primary bunny:full}; do
         IFS=: read scn md <<< "$sc"
         for pol in ${MPOLICIES:-lib moved0 r1 nolpt}; do
           timeout -k 10 180 python tools/moving_ab.py $scn $md $pol 60 2 >> $OUT/moving.jsonl 2>> $OUT/moving.err
           rc=$?; [ $rc -ne 0 ] && { echo "moving $scn $pol rc=$rc"; hard $rc; exit $rc; }
         done
-        if [ -f ray-tracing-project_amd/lib/librtamd_r05.so ]; then
+        if [ -f ray-tracing-project_amd/lib/librtamd_r05.so ] && [ -z "${MNOR05:-}" ]; then
           RTAMD_LIB=$PWD/ray-tracing-project_amd/lib/librtamd_r05.so timeout -k 10 180 python tools/moving_ab.py $scn $md lib 60 2 \
               >> $OUT/moving.jsonl 2>> $OUT/moving.err
           rc=$?; [ $rc -ne 0 ] && { echo "moving r05 $scn rc=$rc"; hard $rc; exit $rc; }
@@ -147,6 +147,17 @@ for s in $STEPS; do
         done
       done
       unset RTAMD_DEBUG_KNOBS ;;
+    tail)
+      # lone-frame tails with the product's split (tools/tail_probe.py) and the hybrid model over the FULL phases
+      export RTAMD_DEBUG_KNOBS=1
+      for c in c5 c3 c2; do
+        RT_TIMELINE_SPLIT=1 timeout -k 10 180 python tools/tail_probe.py $c static moving >> $OUT/tail.jsonl 2>> $OUT/tail.err
+        rc=$?; [ $rc -ne 0 ] && { echo "tail $c rc=$rc"; tail -5 $OUT/tail.err; hard $rc; exit $rc; }
+      done
+      unset RTAMD_DEBUG_KNOBS
+      timeout -k 10 300 python tools/hybrid_model.py bunny:full soup:full > $OUT/hybrid_full.jsonl 2> $OUT/hybrid_full.err
+      rc=$?; echo "hybrid full rc=$rc"; hard $rc
+      cat $OUT/tail.jsonl $OUT/hybrid_full.jsonl ;;
     multi8)
       # eight replicas of the scene sharing the box's GPU: the in-process 8-device path end to end (enqueue workers,
       # assembly); the rate is one GPU's, the line shows the host enqueue cost per frame and per-device figures

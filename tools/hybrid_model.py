@@ -12,7 +12,7 @@ are priced with the per-step costs measured on the product kernels (DESIGN.md se
 19.4 triangle tests), a packet triangle test ~100 VALU + 1 SMEM; a per-lane node step pays the same 12 FMA
 box tests plus the per-lane decision and stack (~34 VALU, the VGPR-stack loop's count) and four vector loads
 of the 64-B record instead of one scalar load; a per-lane triangle test the same ~100 VALU plus four vector
-loads. Usage (GPU box): python tools/hybrid_model.py [soup bunny]"""
+loads. Usage (GPU box): python tools/hybrid_model.py [soup bunny bunny:full]"""
 import json
 import os
 import sys
@@ -38,18 +38,20 @@ L_TRI_VALU, L_TRI_VMEM = 100.0, 4.0
 def main(scenes):
     W, H = 1920, 1080
     out = []
-    for name in scenes:
+    for spec in scenes:
+        name, _, mode = spec.partition(":")  # e.g. bunny:full -- every phase of the FULL megakernel counted together
         if name == "soup":
             mesh, _, _ = rt.soup_mesh(1_000_000, 12345)
         else:
             mesh = rt.Mesh.load_obj(os.path.join(ROOT, "scenes", "bunny.obj"))
         sc = rt.Scene(mesh, device=0)
         cam = rt.flycam(W, H, 0, 0, 20)
-        sc.render(cam, rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS)
+        sc.render(cam, rt.DEFAULT_LIGHTS, W, H, flags=rt.RT_FRAME_STATS,
+                  **({"mode": rt.RT_MODE_FULL} if mode == "full" else {}))
         c = sc.counters(64)
         waves = (W // 8) * ((H + 7) // 8)
         wn, wt = c[ST_WNODE], c[ST_WTRI]
-        d = {"scene": name, "waves": waves, "node_steps_per_wave": wn / waves, "tri_tests_per_wave": wt / waves,
+        d = {"scene": spec, "waves": waves, "node_steps_per_wave": wn / waves, "tri_tests_per_wave": wt / waves,
              "node_visits_per_ray": c[ST_NODE] / c[ST_RAYS], "tri_tests_per_ray": c[ST_TRI] / c[ST_RAYS],
              "node_lanes_hist": {b: c[ST_HN0 + i] / max(wn, 1) for i, b in enumerate(BINS)},
              "leaf_lanes_hist": {b: c[ST_HL0 + i] / max(sum(c[ST_HL0:ST_HL0 + 7]), 1) for i, b in enumerate(BINS)}}

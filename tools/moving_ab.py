@@ -7,9 +7,10 @@ cost maps were per frame slot). One JSON line per measurement.
 
 Usage: RTAMD_DEBUG_KNOBS=1 python tools/moving_ab.py <soup|bunny> <primary|full> <policy> [frames] [reps]
   policy: lib (the library as built), moved0 / moved1 (RT_LPT_MOVED), r1 (RT_LPT_REFRESH=1), nolpt (variant 131072),
-          dil0 / dil1 / dil2 (RT_LPT_DILATE: a moving camera's cost map dilated over r waves), exact (every pose
+          dil0 / dil1 / dil2 (RT_LPT_DILATE: a moving camera's cost map dilated over r waves), nopred (RT_LPT_PRED=0:
+          the map dilated around each wave's own position, not its predicted one), exact (every pose
           rendered twice and the second render timed: its map was recorded at the same pose -- the best an order
-          from wave costs can do on the moving poses)
+          from wave costs can do on the moving poses), env:K=V[,K=V...] (any debug knobs)
 """
 import json
 import os
@@ -25,7 +26,9 @@ frames = int(sys.argv[4]) if len(sys.argv) > 4 else 60
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 2
 env = {"moved0": {"RT_LPT_MOVED": "0"}, "moved1": {"RT_LPT_MOVED": "1"}, "r1": {"RT_LPT_REFRESH": "1"},
        "dil0": {"RT_LPT_DILATE": "0"}, "dil1": {"RT_LPT_DILATE": "1"}, "dil2": {"RT_LPT_DILATE": "2"},
-       "exact": {"RT_LPT_DILATE": "0"}}.get(policy, {})
+       "nopred": {"RT_LPT_PRED": "0"}, "exact": {"RT_LPT_DILATE": "0", "RT_LPT_PRED": "0"}}.get(policy, {})
+if policy.startswith("env:"):  # any debug knobs, e.g. env:RT_SPLIT_KP_ANY=1,RT_LPT_MOVED=1
+    env = dict(kv.split("=", 1) for kv in policy[4:].split(","))
 os.environ.update(env)
 rt = bench.load_rtamd()
 import torch  # noqa: E402

@@ -11,12 +11,12 @@ for line in open(sys.argv[1]):
     if not line.startswith("{"):
         continue
     d = json.loads(line)
-    rows[(d["scene"], d["lib"], d["policy"], d["fif"], d["camera"])].append(d)
-print(f"{'scene':6} {'library':22} {'policy':7} {'slots':5} {'camera':7} {'Mrays/s':>9} {'wall ms':>8} {'kernel ms':>9}  lpt")
+    rows[(d["scene"] + ":" + d.get("mode", ""), d["lib"], d["policy"], d["fif"], d["camera"])].append(d)
+print(f"{'scene':13} {'library':22} {'policy':7} {'slots':5} {'camera':7} {'Mrays/s':>9} {'wall ms':>8} {'kernel ms':>9}  lpt")
 for k in sorted(rows):
     v = rows[k]
     mr = sum(x["mrays_per_s_one_at_a_time"] for x in v) / len(v)
     wm = sum(x["frame_ms_wall"] for x in v) / len(v)
     km = sum(x["kernel_ms"] for x in v) / len(v)
     lpt = v[-1].get("lpt", "")
-    print(f"{k[0]:6} {k[1]:22} {k[2]:7} {k[3]:5} {k[4]:7} {mr:9.1f} {wm:8.4f} {km:9.4f}  {lpt}")
+    print(f"{k[0]:13} {k[1]:22} {k[2]:7} {k[3]:5} {k[4]:7} {mr:9.1f} {wm:8.4f} {km:9.4f}  {lpt}")
