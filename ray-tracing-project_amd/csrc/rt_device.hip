@@ -73,7 +73,9 @@ static void camera_step(const float* vp_prev, const float* v_cur, float* step3) 
 }
 constexpr int kSplitK = 1536;  // FULL lone frames: waves split into 16-lane sub-waves (FrameParams::split_k); round 5
                                // re-sweep without the spill: 1536 +2.5..6% over 2048 (profiles/ab/r05_c5_split_ab.txt)
-constexpr int kSplitKPrimary = 1024;  // the same for k_primary_fused (small scenes)
+constexpr int kSplitKPrimary = 256;   // the same for k_primary_fused (small scenes); round 6 re-sweep after the
+                                      // scene-level map: 256 against 1024 -2.5% static, -7% moving, -8% at a stopped
+                                      // pose (C2 lone frames, profiles/ab/r06_split_size_ab.txt)
 __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c, int shift) {
   // 4 buckets per octave: exponent and 2 mantissa bits of (float)c; costs of 2^10 .. 2^18 shader cycles
   // (0.5 .. 120 us at 2.1 GHz) spread over the buckets, longest first (bucket 0)
